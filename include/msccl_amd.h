@@ -1,0 +1,42 @@
+/*
+ * msccl-amd — introspection C-ABI used by the tests and the benchmark.
+ *
+ * These entry points have no counterpart in the reference's public header; they expose the
+ * host-side pieces of the MSCCL path (XML loader, selection + chunk math, bootstrap) so the
+ * parity tests can compare them with the CPU oracle without a GPU.
+ */
+#ifndef MSCCL_AMD_H_
+#define MSCCL_AMD_H_
+
+#include <stddef.h>
+#include "nccl.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Load one MSCCL XML file as rank `rank` of `nranks` (graph/topo.cc:759-1193) and write the
+ * resulting program as JSON into out[0..outLen).  Returns the ncclResult_t of the load. */
+int mscclAmdAlgoJson(const char* xmlPath, int rank, int nranks, char* out, size_t outLen);
+
+/* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the launch plan
+ * (enqueue.cc:591-734).  coll uses ncclFunc_t numbering (AllGather=2, ReduceScatter=3,
+ * AllReduce=4).  Writes JSON {"algo":i,...} or {"algo":-1}.  No GPU needed. */
+int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_t count, int dtype,
+                     int redop, int inPlace, char* out, size_t outLen);
+
+/* Communicator summary as JSON (algorithms, connections, scratch, FIFO geometry). */
+int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen);
+
+/* Bootstrap only (no GPU): rank 0 passes the id from ncclGetUniqueId; every rank contributes
+ * `bytes` bytes and receives nranks*bytes in `out`. */
+int mscclAmdBootstrapAllgather(const ncclUniqueId* id, int rank, int nranks, const void* mine, size_t bytes,
+                               void* out);
+
+/* Number of thread blocks a launch of algorithm `algoIndex` uses on this rank. */
+int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,108 @@
+// Host communicator (replaces the reference's struct ncclComm, include/comm.h:95-217, for the
+// single-node MSCCL path only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <atomic>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/nccl.h"
+#include "algo.h"
+#include "device/devcomm.h"
+
+namespace msccl {
+
+class Bootstrap;
+
+constexpr uint64_t kCommMagic = 0x6d7363636c616d64ull;  // "msccl amd"
+
+// Connection key: (channel, peer)
+struct ConnKey {
+  int chan, peer;
+  bool operator<(const ConnKey& o) const { return chan != o.chan ? chan < o.chan : peer < o.peer; }
+  bool operator==(const ConnKey& o) const { return chan == o.chan && peer == o.peer; }
+};
+
+// Per-rank transport table exchanged during init: for every (channel, peer) the offsets,
+// inside this rank's transport arena, of the receive FIFOs / tail word (this rank receiving
+// from peer) and of the head word (this rank sending to peer).  -1 = no connection.
+struct PeerOffsets {
+  int64_t recvLL, recvSimple, recvTail, sendHead;
+};
+
+struct DevAlgoHost {
+  DevTbHeader* dTbs = nullptr;
+  char* dBlob = nullptr;
+  int nBlocks = 0;
+};
+
+struct ncclCommImpl;
+}  // namespace msccl
+
+struct ncclComm {
+  uint64_t magic = msccl::kCommMagic;
+  int rank = 0, nRanks = 1, cudaDev = 0;
+  int64_t busId = 0;
+  std::vector<msccl::Algorithm> algos;
+  std::vector<msccl::Registration> regs;
+  std::vector<msccl::DevAlgoHost> devAlgos;
+
+  // transport
+  std::vector<msccl::ConnKey> sendKeys, recvKeys;
+  std::vector<uint8_t> sendProtoMask, recvProtoMask;  // bit p = protocol p used
+  char* arena = nullptr;
+  size_t arenaSize = 0;
+  std::vector<msccl::PeerOffsets> table;              // [32 * nRanks] own table
+  std::vector<char*> peerArena;                        // per rank: mapped arena base
+  std::vector<bool> peerArenaIpc;                      // opened through hipIpcOpenMemHandle
+  msccl::DevSendConn* dSend = nullptr;
+  msccl::DevRecvConn* dRecv = nullptr;
+  int llSlotLines = 0, simpleSlotBytes = 0;
+  int buffSizes[3] = {0, 0, 0};
+
+  // MSCCL state
+  uint64_t* dFlags = nullptr;
+  void* scratch = nullptr;
+  size_t scratchSize = 0;
+  uint32_t workIndex = 1;
+  bool flagsNeedReset = false;
+  msccl::DevComm* dComm = nullptr;
+
+  // failure handling
+  uint32_t* hostAbort = nullptr;   // mapped
+  uint32_t* hostErr = nullptr;     // mapped
+  uint32_t* devAbort = nullptr;
+  uint32_t* devErr = nullptr;
+  double timeoutSec = 60.0;
+  ncclResult_t asyncError = ncclSuccess;
+
+  // rendezvous
+  msccl::Bootstrap* boot = nullptr;
+  bool ownsBoot = false;
+
+  hipStream_t userStream = nullptr;
+  bool userStreamSet = false;
+  hipEvent_t doneEvent = nullptr;
+  std::string lastError;
+};
+
+namespace msccl {
+
+// init.cc
+ncclResult_t commSetupTransport(std::vector<ncclComm*>& comms, Bootstrap* boot);
+ncclResult_t commFree(ncclComm* comm, bool peerBarrier);
+bool commValid(const ncclComm* comm);
+
+// transport.cc
+ncclResult_t transportPlan(ncclComm* comm);                 // keys, arena layout, allocation, own table
+ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
+                              const std::vector<char*>& peerBases);
+ncclResult_t algoUpload(ncclComm* comm);
+
+// enqueue.cc
+int typeSize(ncclDataType_t t);
+
+}  // namespace msccl

@@ -1,0 +1,99 @@
+// Introspection C-ABI (include/msccl_amd.h).
+#include <stdio.h>
+#include <string.h>
+
+#include <sstream>
+
+#include "../../include/msccl_amd.h"
+#include "algo.h"
+#include "bootstrap.h"
+#include "comm.h"
+#include "debug.h"
+#include "plan.h"
+
+using namespace msccl;
+
+static int putOut(const std::string& s, char* out, size_t len) {
+  if (!out || len == 0) return ncclInvalidArgument;
+  if (s.size() + 1 > len) return ncclInvalidArgument;
+  memcpy(out, s.c_str(), s.size() + 1);
+  return 0;
+}
+
+extern "C" {
+
+int mscclAmdAlgoJson(const char* xmlPath, int rank, int nranks, char* out, size_t outLen) {
+  Algorithm a;
+  int r = loadAlgoFromXml(xmlPath, &a, kMaxChannels, rank, nranks);
+  if (r != 0) return r;
+  return putOut(algoToJson(a), out, outLen);
+}
+
+int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_t count, int dtype, int redop,
+                     int inPlace, char* out, size_t outLen) {
+  std::vector<Algorithm> algos;
+  loadAlgosFromXmlFiles(xmlFiles, &algos, kMaxChannels, rank, nranks);
+  CallDesc c;
+  c.coll = coll;
+  c.count = count;
+  c.dtype = dtype;
+  c.redop = redop;
+  c.nRanks = nranks;
+  c.rank = rank;
+  c.inPlace = inPlace != 0;
+  std::vector<Registration> regs;
+  int idx = selectAlgo(algos, regs, c);
+  std::ostringstream o;
+  if (idx < 0) {
+    o << "{\"algo\":-1,\"nalgos\":" << algos.size() << "}";
+    return putOut(o.str(), out, outLen);
+  }
+  Plan p;
+  int r = makePlan(algos, idx, -1, c, &p);
+  if (r != 0) return r;
+  o << "{\"algo\":" << idx << ",\"nalgos\":" << algos.size() << ",\"proto\":" << p.proto
+    << ",\"nthreads\":" << p.refNthreads << ",\"count\":" << p.count << ",\"dtype\":" << p.dtype
+    << ",\"sizeMultiplier\":" << p.sizeMultiplier << ",\"nBytes\":" << p.nBytes
+    << ",\"maxAllowedCount\":" << p.maxAllowedCount << ",\"ncpl\":" << p.nchunksPerLoop
+    << ",\"sizePerChunk\":" << p.sizePerChunk << ",\"chunkSize\":" << p.chunkSize << ",\"minChunk\":" << p.minChunk
+    << ",\"scratchNeeded\":" << p.scratchNeeded << ",\"nIters\":" << p.nIters << "}";
+  return putOut(o.str(), out, outLen);
+}
+
+int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
+  if (!commValid(comm)) return ncclInvalidArgument;
+  std::ostringstream o;
+  o << "{\"rank\":" << comm->rank << ",\"nranks\":" << comm->nRanks << ",\"device\":" << comm->cudaDev
+    << ",\"algos\":[";
+  for (size_t i = 0; i < comm->algos.size(); i++) {
+    const Algorithm& a = comm->algos[i];
+    o << (i ? "," : "") << "{\"name\":\"" << a.name << "\",\"proto\":" << a.proto << ",\"coll\":" << a.coll
+      << ",\"nBlocks\":" << a.nBlocks << ",\"ncpl\":" << a.nchunksPerLoop << ",\"inplace\":" << a.inPlace
+      << ",\"minBytes\":" << a.minBytes << ",\"maxBytes\":" << a.maxBytes << ",\"path\":\"" << a.path << "\"}";
+  }
+  o << "],\"sendConns\":" << comm->sendKeys.size() << ",\"recvConns\":" << comm->recvKeys.size()
+    << ",\"arenaBytes\":" << comm->arenaSize << ",\"scratchBytes\":" << comm->scratchSize
+    << ",\"llSlotLines\":" << comm->llSlotLines << ",\"simpleSlotBytes\":" << comm->simpleSlotBytes
+    << ",\"workIndex\":" << comm->workIndex << "}";
+  return putOut(o.str(), out, outLen);
+}
+
+int mscclAmdBootstrapAllgather(const ncclUniqueId* id, int rank, int nranks, const void* mine, size_t bytes,
+                               void* out) {
+  if (!id) return ncclInvalidArgument;
+  SocketBootstrap* b = nullptr;
+  ncclResult_t r = SocketBootstrap::connect(*id, rank, nranks, &b);
+  if (r != ncclSuccess) return r;
+  std::vector<char> all;
+  r = b->allgather(mine, bytes, &all);
+  if (r == ncclSuccess) memcpy(out, all.data(), all.size());
+  delete b;
+  return r;
+}
+
+int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex) {
+  if (!commValid(comm) || algoIndex < 0 || algoIndex >= (int)comm->algos.size()) return -1;
+  return comm->algos[algoIndex].nBlocks;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// Device-visible data model of the MI355X MSCCL runtime (shared by host C++ and HIP kernels).
+//
+// Replaces the reference's ncclDevComm / ncclConnInfo / mscclThreadBlock device copies
+// (include/devcomm.h:83-295, include/msccl.h:46-118).  Differences by design:
+//   * the per-tb program is a packed blob (16-B transfers + int16 dep/reduction tables)
+//     copied into LDS by each workgroup, instead of a fixed 5,904-B mscclThreadBlock;
+//   * one connection = receiver-owned FIFO in uncached (fine-grained) HBM plus a head word in
+//     the sender's memory and a tail word in the receiver's memory; the sender writes the
+//     FIFO over xGMI (peer pointer or hipIpc mapping);
+//   * a launch may carry the work of several co-resident ranks (ranks that share one GPU):
+//     RankWork[i] owns blocks [blockBase, blockBase + nBlocks).
+#pragma once
+#include <stdint.h>
+
+namespace msccl {
+
+constexpr int kFifoSteps = 8;          // NCCL_STEPS
+constexpr int kMaxLaunchRanks = 16;    // ranks fused into one launch (same device, same group)
+constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag padding)
+constexpr int kFlagSlots = 256;        // >= MSCCL_MAX_NUM_THREAD_BLOCKS
+constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
+
+// LL FIFO line (ncclLLFifoLine, devcomm.h:35-48): two 8-B {4-B data, 4-B flag} granules.
+struct alignas(16) LLLine { uint32_t d0, f0, d1, f1; };
+
+// Packed transfer (mscclTransfer, msccl.h:46-58).
+struct alignas(16) DevTransfer {
+  int16_t srcoff, dstoff;
+  uint8_t srcbuf, dstbuf, type, count;
+  int16_t depPtr, numDeps;
+  int16_t redPtr;
+  uint8_t numReds, hasDep;
+};
+static_assert(sizeof(DevTransfer) == 16, "DevTransfer must be 16 bytes");
+
+struct alignas(16) DevTbHeader {
+  int16_t sendConn, recvConn;   // index into DevComm::send / ::recv, -1 if none
+  uint16_t nsteps, ndeps;
+  uint16_t nreds, pad;
+  uint32_t blobOffset;          // bytes: [nsteps DevTransfer][ndeps int16 bid][ndeps int16 step][nreds int16 off]
+};
+static_assert(sizeof(DevTbHeader) == 16, "DevTbHeader must be 16 bytes");
+
+struct DevSendConn {
+  LLLine* ll;                  // receiver's LL FIFO (peer memory)  [kFifoSteps][llSlotLines]
+  char* simple;                 // receiver's Simple FIFO (peer memory) [kFifoSteps][simpleSlotBytes]
+  uint64_t* remoteTail;         // receiver's tail word (peer memory)
+  uint64_t* head;               // my head word, written by the receiver
+  uint64_t step;                // persistent step counter (owned by one workgroup)
+  int32_t llSlotLines;
+  int32_t simpleSlotBytes;
+};
+
+struct DevRecvConn {
+  LLLine* ll;                  // my LL FIFO
+  char* simple;                 // my Simple FIFO
+  uint64_t* tail;               // my tail word, written by the sender
+  uint64_t* remoteHead;         // sender's head word (peer memory)
+  uint64_t step;
+  int32_t llSlotLines;
+  int32_t simpleSlotBytes;
+};
+
+struct DevComm {
+  DevSendConn* send;
+  DevRecvConn* recv;
+  uint64_t* flags;              // [kFlagSlots * kFlagStride]
+  volatile uint32_t* abortFlag; // host-mapped
+  uint32_t* errWord;            // host-mapped: 0 ok, else error code (1 timeout, 2 bad program)
+  uint64_t timeoutTicks;        // s_memrealtime ticks (100 MHz)
+};
+
+// One rank's share of a launch (the reference passes ncclDevComm* + a 64-B ncclWorkElem,
+// common.h:263-266; here the whole descriptor rides in the kernel argument block).
+struct RankWork {
+  const void* sendbuff;
+  void* recvbuff;
+  void* scratch;
+  DevComm* comm;
+  const DevTbHeader* tbs;
+  const char* blob;
+  int64_t sizePerChunk;         // sizePerMscclChunk = count*sizeMultiplier/nchunksPerLoop (elements)
+  int64_t chunkSize;            // interpreter chunkSize (elements)
+  int64_t minChunk;             // LL: nthreads*8/sizeof(T); Simple: rounding unit (nthreads-32)*8/sizeof(T)
+  uint32_t workIndex;
+  int16_t blockBase;
+  int16_t nBlocks;
+  int16_t refNthreads;          // reference nthreads (small-reduce switch, chunk rounding)
+  uint8_t maxAllowedCount;
+  uint8_t pad;
+};
+
+struct LaunchArgs {
+  int32_t nRanks;
+  int32_t pad;
+  RankWork w[kMaxLaunchRanks];
+};
+
+// Error codes in DevComm::errWord
+enum : uint32_t { kDevOk = 0, kDevTimeout = 1, kDevAbort = 2, kDevBadOp = 3 };
+
+// Host-side kernel dispatch (kernels.hip)
+typedef int (*LaunchFn)(const LaunchArgs& args, int gridBlocks, void* stream);
+LaunchFn getLaunchFn(int dtype, int redop, int proto);
+
+}  // namespace msccl

@@ -1,0 +1,410 @@
+// MSCCL schedule interpreter for gfx950 (one workgroup = one XML thread block).
+//
+// Behaviour follows the reference interpreter collectives/device/msccl_interpreter.h:66-205:
+//   * outer loop over gridOffset in steps of chunkSize; per-protocol realChunkSize/nelem
+//     (msccl_interpreter.h:105-113);
+//   * per transfer: wait on dependency flags COMPUTE_FLAG(workIndex, iter, step) of other
+//     workgroups of the same rank (123-140), split `count` by mscclMaxAllowedCount (146-150),
+//     dispatch to the primitive, publish the own flag when hasdep (198-201);
+//   * reductions: LL order d(+)s0(+)s1.. (prims_ll.h:347-362), Simple order (s0(+)s1..)(+)d
+//     (prims_simple.h:258-263), per-element d-first path when thisNelem < nthreads (157-170);
+//   * recv-reduce: LL fn(peer, local) (prims_ll.h:282-287), Simple fn(local, peer).
+// Implementation is MI355X-native: wave64 workgroups of kNT threads, 16-B packs per lane,
+// buffer loads/stores with explicit cache-policy bits, LL lines polled two at a time with a
+// single wait, FIFO flow control with head/tail words in uncached memory, bounded spins.
+#pragma once
+#include "primitives.h"
+
+namespace msccl {
+
+enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7 };
+enum : int { pLL = 0, pLL128 = 1, pSimple = 2 };
+constexpr uint64_t kLLCleanMask = 0x7ffffff8ull;  // NCCL_LL_CLEAN_MASK (devcomm.h:61)
+
+struct alignas(16) BlockShared {
+  DevTransfer tr[256];
+  int16_t depBid[256];
+  int16_t depStep[256];
+  int16_t red[256];
+  uint64_t step[2];
+  uint32_t aborted;
+};
+
+__device__ __forceinline__ uint64_t computeFlag(uint64_t workIndex, uint64_t iter, uint64_t step) {
+  return workIndex * (65536ull * 256ull) + iter * 256ull + step;  // msccl_interpreter.h:14-16
+}
+
+// LL line index of (pack p, half h): each group of 64 packs stores its first lines in 64
+// consecutive lines and its second lines in the next 64, so a wave's stores/loads of one half
+// are a contiguous 1 KiB.
+__device__ __forceinline__ int llLineIdx(int p, int h) { return ((p >> 6) << 7) + (h << 6) + (p & 63); }
+
+template <typename T, int OP, int PROTO>
+struct Interp {
+  using F = Fn<T, OP>;
+  static constexpr int TS = sizeof(T);
+  static constexpr int PE = 16 / TS;  // elements per 16-B pack
+
+  BlockShared* sh;
+  DevComm* comm;
+  DevSendConn* sc;
+  DevRecvConn* rc;
+  uint64_t sendStep, recvStep;
+  uint64_t t0;
+  int tid;
+  int refNthreads;
+
+  // ---------------------------------------------------------------- spins / abort
+  __device__ __forceinline__ bool spinAbort(uint32_t& spins) {
+    if ((++spins & 1023u) != 0) return false;
+    if (sh->aborted) return true;
+    uint32_t code = kDevOk;
+    if (*comm->abortFlag) code = kDevAbort;
+    else if (__builtin_amdgcn_s_memrealtime() - t0 > comm->timeoutTicks) code = kDevTimeout;
+    if (code != kDevOk) {
+      sh->aborted = 1;
+      __hip_atomic_store(comm->errWord, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+    return false;
+  }
+
+  __device__ __forceinline__ void waitSendCredit() {
+    if (tid == 0) {
+      uint32_t spins = 0;
+      while (atomicLoadSys(sc->head) + kFifoSteps < sendStep + 1) {
+        if (spinAbort(spins)) break;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- pack helpers
+  __device__ __forceinline__ u32x4 loadPartial(__amdgpu_buffer_rsrc_t r, int e0, int ne) {
+    T v[PE];
+#pragma unroll
+    for (int i = 0; i < PE; i++) {
+      if (i < ne) v[i] = ldElem<T>(r, (uint32_t)(e0 + i) * TS);
+      else __builtin_memset(&v[i], 0, TS);
+    }
+    u32x4 o;
+    __builtin_memcpy(&o, v, 16);
+    return o;
+  }
+  __device__ __forceinline__ void storePartial(__amdgpu_buffer_rsrc_t r, int e0, int ne, u32x4 x) {
+    T v[PE];
+    __builtin_memcpy(v, &x, 16);
+#pragma unroll
+    for (int i = 0; i < PE; i++)
+      if (i < ne) stElem<T>(r, (uint32_t)(e0 + i) * TS, v[i]);
+  }
+  __device__ __forceinline__ u32x4 loadPack(__amdgpu_buffer_rsrc_t r, bool vec, int p, int nelem) {
+    int e0 = p * PE;
+    int ne = nelem - e0;
+    if (vec && ne >= PE) return ld16<kAuxLocal>(r, (uint32_t)e0 * TS);
+    return loadPartial(r, e0, ne < PE ? ne : PE);
+  }
+  __device__ __forceinline__ void storePack(__amdgpu_buffer_rsrc_t r, bool vec, int p, int nelem, u32x4 x) {
+    int e0 = p * PE;
+    int ne = nelem - e0;
+    if (vec && ne >= PE) st16<kAuxLocal>(r, (uint32_t)e0 * TS, x);
+    else storePartial(r, e0, ne < PE ? ne : PE, x);
+  }
+  static __device__ __forceinline__ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+  // ---------------------------------------------------------------- LL protocol
+  template <int RECV, int SEND, int SRC, int DST>
+  __device__ void llOp(const T* src, T* dst, int nelem) {
+    constexpr int E = 8 / TS;  // elements per line
+    const int nlines = (nelem + E - 1) / E;
+    const int npacks = (nlines + 1) / 2;
+    if (SEND) waitSendCredit();
+    LLLine* rslot = nullptr;
+    __amdgpu_buffer_rsrc_t srs, drs, frs;
+    uint32_t rflag = 0, sflag = 0;
+    if (RECV) {
+      rslot = rc->ll + (recvStep % kFifoSteps) * (uint64_t)rc->llSlotLines;
+      rflag = (uint32_t)(recvStep + 1);
+    }
+    if (SEND) {
+      frs = makeRsrc(sc->ll + (sendStep % kFifoSteps) * (uint64_t)sc->llSlotLines);
+      sflag = (uint32_t)(sendStep + 1);
+    }
+    if (SRC) srs = makeRsrc(src);
+    if (DST) drs = makeRsrc(dst);
+    const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
+    for (int p = tid; p < npacks; p += kNT) {
+      const int l0 = llLineIdx(p, 0), l1 = llLineIdx(p, 1);
+      const bool two = 2 * p + 1 < nlines;
+      u32x4 data = {0, 0, 0, 0}, v;
+      if (SRC) data = loadPack(srs, vec, p, nelem);
+      if (RECV) {
+        u32x4 a, b = {0, 0, 0, 0};
+        uint32_t spins = 0;
+        if (two) {
+          do {
+            ldLines2(rslot + l0, rslot + l1, a, b);
+          } while ((a.y != rflag || a.w != rflag || b.y != rflag || b.w != rflag) && !spinAbort(spins));
+        } else {
+          do {
+            ldLine1(rslot + l0, a);
+          } while ((a.y != rflag || a.w != rflag) && !spinAbort(spins));
+        }
+        u32x4 peer = {a.x, a.z, b.x, b.z};
+        v = SRC ? F::pack(peer, data) : peer;
+      } else {
+        v = data;
+      }
+      if (SEND) {
+        st16<kAuxFifo>(frs, (uint32_t)l0 * 16, (u32x4){v.x, sflag, v.y, sflag});
+        if (two) st16<kAuxFifo>(frs, (uint32_t)l1 * 16, (u32x4){v.z, sflag, v.w, sflag});
+      }
+      if (DST) storePack(drs, vec, p, nelem, v);
+    }
+    if (SEND) {
+      if ((sendStep & kLLCleanMask) == kLLCleanMask) {
+        // LL cleanup (prims_ll.h:90-97): stamp every unused line of the slot with this flag
+        for (int l = tid; l < sc->llSlotLines; l += kNT) {
+          int p = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
+          if (2 * p + h >= nlines) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
+        }
+      }
+      sendStep++;
+    }
+    if (RECV) {
+      recvStep++;
+      __syncthreads();
+      if (tid == 0) atomicStoreSys(rc->remoteHead, recvStep);
+    }
+  }
+
+  // ---------------------------------------------------------------- Simple protocol
+  template <int RECV, int SEND, int SRC, int DST>
+  __device__ void simpleOp(const T* src, T* dst, int nelem) {
+    const int slotBytes = SEND ? sc->simpleSlotBytes : rc->simpleSlotBytes;
+    const int sliceElems = slotBytes / TS;
+    for (int off = 0; off < nelem; off += sliceElems) {
+      const int n = nelem - off < sliceElems ? nelem - off : sliceElems;
+      if (tid == 0) {
+        uint32_t spins = 0;
+        if (RECV)
+          while (atomicLoadSys(rc->tail) < recvStep + 1)
+            if (spinAbort(spins)) break;
+        if (SEND)
+          while (atomicLoadSys(sc->head) + kFifoSteps < sendStep + 1)
+            if (spinAbort(spins)) break;
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      __amdgpu_buffer_rsrc_t srs, drs, rrs, frs;
+      if (SRC) srs = makeRsrc(src + off);
+      if (DST) drs = makeRsrc(dst + off);
+      if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
+      if (SEND) frs = makeRsrc(sc->simple + (sendStep % kFifoSteps) * (uint64_t)slotBytes);
+      const bool vec = (!SRC || aligned16(src + off)) && (!DST || aligned16(dst + off));
+      const int npacks = (n + PE - 1) / PE;
+      for (int p = tid; p < npacks; p += kNT) {
+        u32x4 data = {0, 0, 0, 0}, v;
+        if (SRC) data = loadPack(srs, vec, p, n);
+        if (RECV) {
+          u32x4 peer = ld16<kAuxFifo>(rrs, (uint32_t)p * 16);
+          v = SRC ? F::pack(data, peer) : peer;
+        } else {
+          v = data;
+        }
+        if (SEND) st16<kAuxFifo>(frs, (uint32_t)p * 16, v);
+        if (DST) storePack(drs, vec, p, n, v);
+      }
+      drainStores();
+      __syncthreads();
+      if (tid == 0) {
+        if (SEND) atomicStoreSys(sc->remoteTail, sendStep + 1);
+        if (RECV) atomicStoreSys(rc->remoteHead, recvStep + 1);
+      }
+      if (SEND) sendStep++;
+      if (RECV) recvStep++;
+    }
+  }
+
+  template <int RECV, int SEND, int SRC, int DST>
+  __device__ __forceinline__ void op(const T* src, T* dst, int nelem) {
+    if constexpr (PROTO == pSimple) simpleOp<RECV, SEND, SRC, DST>(src, dst, nelem);
+    else llOp<RECV, SEND, SRC, DST>(src, dst, nelem);
+  }
+
+  // ---------------------------------------------------------------- local ops
+  __device__ void localCopy(const T* src, T* dst, int nelem) {
+    __amdgpu_buffer_rsrc_t srs = makeRsrc(src), drs = makeRsrc(dst);
+    const bool vec = aligned16(src) && aligned16(dst);
+    const int npacks = (nelem + PE - 1) / PE;
+    for (int p = tid; p < npacks; p += kNT) storePack(drs, vec, p, nelem, loadPack(srs, vec, p, nelem));
+  }
+
+  // srcOffs[r] are element offsets from srcBase; MSCCL_MAX_REDUCE_FUSION = 16
+  __device__ void reduce(const T* srcBase, const int64_t* srcOffs, int nsrc, T* dst, int nelem) {
+    if (nelem < refNthreads) {
+      // per-element path, d first: o = fn(s_r, o) (msccl_interpreter.h:157-170)
+      __amdgpu_buffer_rsrc_t drs = makeRsrc(dst), srs = makeRsrc(srcBase);
+      for (int e = tid; e < nelem; e += kNT) {
+        T o = ldElem<T>(drs, (uint32_t)e * TS);
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+          if (r < nsrc) o = F::elem(ldElem<T>(srs, (uint32_t)(srcOffs[r] + e) * TS), o);
+        stElem<T>(drs, (uint32_t)e * TS, o);
+      }
+      return;
+    }
+    __amdgpu_buffer_rsrc_t drs = makeRsrc(dst);
+    bool vec = aligned16(dst);
+#pragma unroll
+    for (int r = 0; r < 16; r++)
+      if (r < nsrc) vec = vec && aligned16(srcBase + srcOffs[r]);
+    const int npacks = (nelem + PE - 1) / PE;
+    for (int p = tid; p < npacks; p += kNT) {
+      u32x4 d = loadPack(drs, vec, p, nelem);
+      u32x4 acc;
+      if constexpr (PROTO == pSimple) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          if (r < nsrc) {
+            u32x4 s = loadPack(makeRsrc(srcBase + srcOffs[r]), vec, p, nelem);
+            acc = r == 0 ? s : F::pack(acc, s);
+          }
+        }
+        acc = F::pack(acc, d);
+      } else {
+        acc = d;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          if (r < nsrc) acc = F::pack(acc, loadPack(makeRsrc(srcBase + srcOffs[r]), vec, p, nelem));
+        }
+      }
+      storePack(drs, vec, p, nelem, acc);
+    }
+  }
+
+  // ---------------------------------------------------------------- the interpreter loop
+  __device__ void run(const RankWork& w, int bid) {
+    tid = threadIdx.x;
+    comm = w.comm;
+    refNthreads = w.refNthreads;
+    t0 = __builtin_amdgcn_s_memrealtime();
+    const DevTbHeader hd = w.tbs[bid];
+    // stage the tb program in LDS
+    const DevTransfer* gtr = (const DevTransfer*)(w.blob + hd.blobOffset);
+    const int16_t* gdep = (const int16_t*)(gtr + hd.nsteps);
+    for (int i = tid; i < hd.nsteps; i += kNT) sh->tr[i] = gtr[i];
+    for (int i = tid; i < hd.ndeps; i += kNT) {
+      sh->depBid[i] = gdep[i];
+      sh->depStep[i] = gdep[hd.ndeps + i];
+    }
+    for (int i = tid; i < hd.nreds; i += kNT) sh->red[i] = gdep[2 * hd.ndeps + i];
+    sc = hd.sendConn >= 0 ? comm->send + hd.sendConn : nullptr;
+    rc = hd.recvConn >= 0 ? comm->recv + hd.recvConn : nullptr;
+    if (tid == 0) {
+      sh->step[0] = sc ? sc->step : 0;
+      sh->step[1] = rc ? rc->step : 0;
+      sh->aborted = 0;
+    }
+    __syncthreads();
+    sendStep = sh->step[0];
+    recvStep = sh->step[1];
+
+    T* thisInput = (T*)w.sendbuff;
+    T* thisOutput = (T*)w.recvbuff;
+    T* thisScratch = (T*)w.scratch;
+    const int64_t sizePer = w.sizePerChunk;
+    const int64_t chunkSize = w.chunkSize;
+    const int mac = w.maxAllowedCount;
+    const uint64_t workIndex = w.workIndex;
+    uint64_t* flags = comm->flags;
+    bool stop = false;
+
+    for (int64_t grid = 0, iter = 0; grid < sizePer && !stop; grid += chunkSize, iter++) {
+      int64_t real;
+      if constexpr (PROTO == pSimple) {
+        real = sizePer - grid < chunkSize ? sizePer - grid : chunkSize;
+        real = (real + w.minChunk - 1) / w.minChunk * w.minChunk;
+      } else {
+        int64_t rem = (sizePer - grid + w.minChunk - 1) / w.minChunk * w.minChunk;
+        real = rem < chunkSize ? rem : chunkSize;
+      }
+      real = (int)real;
+      const int nelem = (int)(real < sizePer - grid ? real : sizePer - grid);
+      int step = 0;
+      for (int i = 0; i < hd.nsteps; i++) {
+        const DevTransfer t = sh->tr[i];
+        if (t.numDeps > 0) {
+          if (tid < t.numDeps) {
+            const int db = sh->depBid[t.depPtr + tid];
+            const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)sh->depStep[t.depPtr + tid]);
+            uint32_t spins = 0;
+            while (true) {
+              uint64_t cur = atomicLoadAgent(flags + (size_t)db * kFlagStride);
+              if (cur >= goal && (cur >> 24) == workIndex) break;
+              if (spinAbort(spins)) break;
+            }
+          }
+          step += t.numDeps - 1;
+          __syncthreads();
+        }
+        T* srcP = t.srcbuf == 0 ? thisInput : (t.srcbuf == 1 ? thisOutput : thisScratch);
+        T* dstP = t.dstbuf == 0 ? thisInput : (t.dstbuf == 1 ? thisOutput : thisScratch);
+        for (int c = 0; c < t.count; c += mac) {
+          const int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
+          const int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;
+          const int thisCount = mac < t.count - c ? mac : t.count - c;
+          const int n = nelem * thisCount;
+          switch (t.type) {
+            case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, n); __syncthreads(); break;
+            case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, n); break;
+            case tRCS: op<1, 1, 0, 1>(nullptr, dstP + dstoff, n); break;
+            case tRRS: op<1, 1, 1, 0>(srcP + srcoff, nullptr, n); break;
+            case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, n); break;
+            case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, n); break;
+            case tCpy: localCopy(srcP + srcoff, dstP + dstoff, n); __syncthreads(); break;
+            case tRe: {
+              int64_t offs[16];
+#pragma unroll
+              for (int r = 0; r < 16; r++)
+                offs[r] = r < t.numReds ? grid + (int64_t)(sh->red[t.redPtr + r] + c) * sizePer : 0;
+              reduce(srcP, offs, t.numReds, dstP + dstoff, n);
+              if (c == 0) step += t.numReds - 1;
+              __syncthreads();
+              break;
+            }
+            default: stop = true; break;  // MSCCL_RES_ADD / unknown: the tb ends (interpreter.h:195-196)
+          }
+          if (stop) break;
+        }
+        if (stop) break;
+        if (t.hasDep) {
+          drainStores();
+          __syncthreads();
+          if (tid == 0) atomicStoreAgent(flags + (size_t)bid * kFlagStride, computeFlag(workIndex, iter, step));
+        }
+        step++;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (sc) sc->step = sendStep;
+      if (rc) rc->step = recvStep;
+    }
+  }
+};
+
+template <typename T, int OP, int PROTO>
+__global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
+  __shared__ BlockShared sh;
+  int b = blockIdx.x;
+  int r = 0;
+  while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
+  const RankWork& w = args.w[r];
+  Interp<T, OP, PROTO> it;
+  it.sh = &sh;
+  it.run(w, b - w.blockBase);
+}
+
+}  // namespace msccl

@@ -1,0 +1,21 @@
+// Kernel instantiation + host launch shim (one translation unit per element type so the
+// 80 kernels build in parallel).
+#pragma once
+#include "interpreter.h"
+
+namespace msccl {
+
+template <typename T, int OP, int PROTO>
+int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  hipLaunchKernelGGL((mscclKernel<T, OP, PROTO>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, args);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+#define MSCCL_DEFINE_TABLE(NAME, T)                                                      \
+  LaunchFn NAME[4][3] = {                                                                \
+      {launchKernel<T, kSum, pLL>, nullptr, launchKernel<T, kSum, pSimple>},             \
+      {launchKernel<T, kProd, pLL>, nullptr, launchKernel<T, kProd, pSimple>},           \
+      {launchKernel<T, kMax, pLL>, nullptr, launchKernel<T, kMax, pSimple>},             \
+      {launchKernel<T, kMin, pLL>, nullptr, launchKernel<T, kMin, pSimple>}};
+
+}  // namespace msccl

@@ -1,0 +1,239 @@
+// Memory-access helpers and elementwise reduction functors for the gfx950 MSCCL kernels.
+//
+// Reduction semantics follow the reference functors (collectives/device/reduce_kernel.h):
+//   Sum/Prod/Max/Min (23-51), FuncSum<half> with the sm_80 +-65504 clamp (244-278),
+//   FuncSum<bf16> = bf16 RNE of the exact sum (280-303), half/bf16 Prod/Max/Min (305-440),
+//   float/double Max/Min = fmax/fmin (442-470), integer types wrap (64-230).
+// fp16 is added with v_pk_add_f16 (correctly rounded) and clamped with v_pk_max/min_f16;
+// bf16 is widened to fp32, added and rounded once with v_cvt_pk_bf16_f32 (RNE): for a sum of
+// two 8-bit-significand values an fp32 intermediate makes the double rounding innocuous.
+//
+// Cache policy (gfx950 CPol bits: sc0=1, nt=2, sc1=16):
+//   local buffers (user input/output/scratch) are read and written with sc1 (device scope)
+//   so that a hand-off between workgroups through a dependency flag needs no L2/L1
+//   maintenance fence (MI355X guide, inter-workgroup visibility, "sc1 stores + sc1 loads");
+//   FIFOs live in uncached fine-grained memory of the receiver and are accessed sc0|sc1.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "devcomm.h"
+
+namespace msccl {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kAuxLocal = 16;   // sc1
+constexpr int kAuxFifo = 17;    // sc0 | sc1
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t makeRsrc(const void* p) {
+  uint64_t a = (uint64_t)p;
+  uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7fffffff, 0x00020000);
+}
+
+template <int AUX>
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, AUX);
+}
+
+// Element loads/stores for tails and unaligned buffers.
+template <typename T>
+__device__ __forceinline__ T ldElem(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  if constexpr (sizeof(T) == 1) {
+    uint8_t v = __builtin_amdgcn_raw_buffer_load_b8(r, off, 0, kAuxLocal);
+    return __builtin_bit_cast(T, v);
+  } else if constexpr (sizeof(T) == 2) {
+    uint16_t v = __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, kAuxLocal);
+    return __builtin_bit_cast(T, v);
+  } else if constexpr (sizeof(T) == 4) {
+    uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, kAuxLocal);
+    return __builtin_bit_cast(T, v);
+  } else {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, kAuxLocal);
+    return __builtin_bit_cast(T, v);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void stElem(__amdgpu_buffer_rsrc_t r, uint32_t off, T x) {
+  if constexpr (sizeof(T) == 1) {
+    __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(uint8_t, x), r, off, 0, kAuxLocal);
+  } else if constexpr (sizeof(T) == 2) {
+    __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(uint16_t, x), r, off, 0, kAuxLocal);
+  } else if constexpr (sizeof(T) == 4) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, x), r, off, 0, kAuxLocal);
+  } else {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, x), r, off, 0, kAuxLocal);
+  }
+}
+
+// Two FIFO lines polled together: both loads in flight, one wait (form (i) of the guide's
+// inline-asm rules: the loads and their s_waitcnt in one statement, early-clobber outputs).
+__device__ __forceinline__ void ldLines2(const void* a, const void* b, u32x4& x, u32x4& y) {
+  asm volatile(
+      "global_load_dwordx4 %0, %2, off sc0 sc1\n\t"
+      "global_load_dwordx4 %1, %3, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x), "=&v"(y)
+      : "v"(a), "v"(b)
+      : "memory");
+}
+__device__ __forceinline__ void ldLine1(const void* a, u32x4& x) {
+  asm volatile(
+      "global_load_dwordx4 %0, %1, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x)
+      : "v"(a)
+      : "memory");
+}
+
+__device__ __forceinline__ uint64_t atomicLoadSys(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void atomicStoreSys(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t atomicLoadAgent(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void atomicStoreAgent(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------------------------------------
+// Elementwise functors.  fn(x, y) keeps the reference's operand order.
+enum RedOp { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
+
+template <typename T> struct IsHalf { static constexpr bool v = false; };
+template <> struct IsHalf<_Float16> { static constexpr bool v = true; };
+
+struct Bf16 { uint16_t bits; };  // bf16 storage type
+
+template <typename T, int OP>
+struct Fn {
+  __device__ __forceinline__ static T elem(T x, T y) {
+    using U = typename std::make_unsigned<T>::type;  // two's-complement wrap, no signed-overflow UB
+    if constexpr (OP == kSum) return (T)(U)((U)x + (U)y);
+    else if constexpr (OP == kProd) return (T)(U)((U)x * (U)y);
+    else if constexpr (OP == kMax) return (x < y) ? y : x;
+    else return (x < y) ? x : y;
+  }
+  __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
+    constexpr int N = 16 / sizeof(T);
+    T xa[N], xb[N];
+    __builtin_memcpy(xa, &a, 16);
+    __builtin_memcpy(xb, &b, 16);
+#pragma unroll
+    for (int i = 0; i < N; i++) xa[i] = elem(xa[i], xb[i]);
+    u32x4 r;
+    __builtin_memcpy(&r, xa, 16);
+    return r;
+  }
+};
+
+template <int OP>
+struct Fn<float, OP> {
+  __device__ __forceinline__ static float elem(float x, float y) {
+    if constexpr (OP == kSum) return x + y;
+    else if constexpr (OP == kProd) return x * y;
+    else if constexpr (OP == kMax) return __builtin_fmaxf(x, y);
+    else return __builtin_fminf(x, y);
+  }
+  __device__ __forceinline__ static uint32_t e1(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, elem(__builtin_bit_cast(float, a), __builtin_bit_cast(float, b)));
+  }
+  __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
+    return (u32x4){e1(a.x, b.x), e1(a.y, b.y), e1(a.z, b.z), e1(a.w, b.w)};
+  }
+};
+
+template <int OP>
+struct Fn<double, OP> {
+  __device__ __forceinline__ static double elem(double x, double y) {
+    if constexpr (OP == kSum) return x + y;
+    else if constexpr (OP == kProd) return x * y;
+    else if constexpr (OP == kMax) return __builtin_fmax(x, y);
+    else return __builtin_fmin(x, y);
+  }
+  __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
+    double xa[2], xb[2];
+    __builtin_memcpy(xa, &a, 16);
+    __builtin_memcpy(xb, &b, 16);
+    xa[0] = elem(xa[0], xb[0]);
+    xa[1] = elem(xa[1], xb[1]);
+    u32x4 r;
+    __builtin_memcpy(&r, xa, 16);
+    return r;
+  }
+};
+
+template <int OP>
+struct Fn<_Float16, OP> {
+  __device__ __forceinline__ static f16x2 op2(f16x2 x, f16x2 y) {
+    if constexpr (OP == kSum) {
+      f16x2 r = x + y;  // v_pk_add_f16, RNE
+      r = __builtin_elementwise_max(r, (f16x2){(_Float16)-65504.0f, (_Float16)-65504.0f});
+      r = __builtin_elementwise_min(r, (f16x2){(_Float16)65504.0f, (_Float16)65504.0f});
+      return r;
+    } else if constexpr (OP == kProd) {
+      return x * y;
+    } else {
+      f32x2 fx = __builtin_convertvector(x, f32x2), fy = __builtin_convertvector(y, f32x2);
+      f32x2 m;
+      if constexpr (OP == kMax) m = (f32x2){__builtin_fmaxf(fx[0], fy[0]), __builtin_fmaxf(fx[1], fy[1])};
+      else m = (f32x2){__builtin_fminf(fx[0], fy[0]), __builtin_fminf(fx[1], fy[1])};
+      return __builtin_convertvector(m, f16x2);
+    }
+  }
+  __device__ __forceinline__ static _Float16 elem(_Float16 x, _Float16 y) {
+    f16x2 r = op2((f16x2){x, x}, (f16x2){y, y});
+    return r[0];
+  }
+  __device__ __forceinline__ static uint32_t e1(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, op2(__builtin_bit_cast(f16x2, a), __builtin_bit_cast(f16x2, b)));
+  }
+  __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
+    return (u32x4){e1(a.x, b.x), e1(a.y, b.y), e1(a.z, b.z), e1(a.w, b.w)};
+  }
+};
+
+template <int OP>
+struct Fn<Bf16, OP> {
+  __device__ __forceinline__ static bf16x2 op2(bf16x2 x, bf16x2 y) {
+    f32x2 fx = __builtin_convertvector(x, f32x2), fy = __builtin_convertvector(y, f32x2);
+    f32x2 r;
+    if constexpr (OP == kSum) r = fx + fy;
+    else if constexpr (OP == kProd) r = fx * fy;
+    else if constexpr (OP == kMax) r = (f32x2){__builtin_fmaxf(fx[0], fy[0]), __builtin_fmaxf(fx[1], fy[1])};
+    else r = (f32x2){__builtin_fminf(fx[0], fy[0]), __builtin_fminf(fx[1], fy[1])};
+    return __builtin_convertvector(r, bf16x2);  // v_cvt_pk_bf16_f32 (RNE)
+  }
+  __device__ __forceinline__ static Bf16 elem(Bf16 x, Bf16 y) {
+    uint32_t ux = x.bits * 0x10001u, uy = y.bits * 0x10001u;
+    bf16x2 r = op2(__builtin_bit_cast(bf16x2, ux), __builtin_bit_cast(bf16x2, uy));
+    Bf16 o;
+    o.bits = (uint16_t)__builtin_bit_cast(uint32_t, r);
+    return o;
+  }
+  __device__ __forceinline__ static uint32_t e1(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, op2(__builtin_bit_cast(bf16x2, a), __builtin_bit_cast(bf16x2, b)));
+  }
+  __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
+    return (u32x4){e1(a.x, b.x), e1(a.y, b.y), e1(a.z, b.z), e1(a.w, b.w)};
+  }
+};
+
+}  // namespace msccl

@@ -1,0 +1,314 @@
+// Collective entry points, group handling and kernel launch.
+//
+// Replaces the reference's host path for the MSCCL algorithm:
+//   collectives/all_reduce.cc:11-19, reduce_scatter.cc:12-20, all_gather.cc:12-20,
+//   all_to_all.cc, custom_collective.cc  ->  enqueue
+//   ncclEnqueueCheck (enqueue.cc:1456-1527), ncclSetupCollKernel (809-866), computeColl
+//   (591-734), ncclLaunchKernel (337-378), nRanks==1 memcpy path (811-816), workIndex/flag
+//   reset (714-721), group.cc:95-408.
+// One fused launch per (device, kernel variant) and group round: a rank's thread blocks
+// occupy blocks [blockBase, blockBase + nBlocks) of the grid.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <map>
+#include <thread>
+#include <vector>
+
+#include "comm.h"
+#include "debug.h"
+#include "group.h"
+#include "plan.h"
+
+namespace msccl {
+
+namespace {
+thread_local int tGroupDepth = 0;
+thread_local std::vector<CollOp> tOps;
+thread_local std::vector<std::pair<std::function<ncclResult_t()>, ncclComm*>> tInits;
+thread_local ncclResult_t tGroupError = ncclSuccess;
+
+struct EventPool {
+  std::vector<hipEvent_t> evs;
+  size_t used = 0;
+  hipEvent_t get() {
+    if (used == evs.size()) {
+      hipEvent_t e;
+      hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      evs.push_back(e);
+    }
+    return evs[used++];
+  }
+};
+thread_local std::map<int, EventPool> tEvents;  // per device
+
+struct Planned {
+  CollOp op;
+  Plan plan;
+  bool memcpyOnly = false;
+  size_t copyBytes = 0;
+  bool noop = false;
+};
+
+ncclResult_t planOp(const CollOp& op, Planned* out) {
+  ncclComm* comm = op.comm;
+  out->op = op;
+  int ts = refTypeSize(op.dtype);
+  if (op.count == 0) { out->noop = true; return ncclSuccess; }
+  if (comm->nRanks == 1) {
+    // enqueue.cc:811-816: one rank = device-to-device copy (or nothing when in place)
+    out->memcpyOnly = true;
+    out->copyBytes = op.count * (size_t)ts;
+    if (op.sendbuff == op.recvbuff) out->noop = true;
+    return ncclSuccess;
+  }
+  CallDesc c;
+  c.coll = op.coll;
+  c.count = op.count;
+  c.dtype = op.dtype;
+  c.redop = op.op;
+  c.nRanks = comm->nRanks;
+  c.rank = comm->rank;
+  c.inPlace = inPlaceOf(op.coll, op.sendbuff, op.recvbuff, op.count, op.dtype, comm->rank);
+  c.customAlgo = op.customAlgo;
+  int idx = selectAlgo(comm->algos, comm->regs, c);
+  if (idx < 0) {
+    WARN("MSCCL: no loaded algorithm matches coll=%d count=%zu type=%d op=%d inplace=%d nranks=%d "
+         "(the reference would fall back to NCCL ring/tree, which this build does not provide)",
+         op.coll, op.count, (int)op.dtype, (int)op.op, (int)c.inPlace, comm->nRanks);
+    return ncclInvalidUsage;
+  }
+  int protoOverride = -1;
+  for (auto& r : comm->regs)
+    if (r.algoIndex == idx) protoOverride = r.proto;
+  NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, &out->plan));
+  if (out->plan.proto == kProtoLL128) out->plan.proto = kProtoLL;  // LL128 schedules run on the LL path
+  if (out->plan.scratchNeeded > comm->scratchSize) {
+    WARN("MSCCL: MSCCL scratch pad size is smaller than expected %zu < %zu", comm->scratchSize, out->plan.scratchNeeded);
+    return ncclInternalError;
+  }
+  return ncclSuccess;
+}
+
+RankWork makeWork(Planned& p) {
+  ncclComm* comm = p.op.comm;
+  const DevAlgoHost& da = comm->devAlgos[p.plan.algoIndex];
+  RankWork w;
+  memset(&w, 0, sizeof(w));
+  w.sendbuff = p.op.sendbuff;
+  w.recvbuff = p.op.recvbuff;
+  w.scratch = comm->scratch;
+  w.comm = comm->dComm;
+  w.tbs = da.dTbs;
+  w.blob = da.dBlob;
+  w.sizePerChunk = p.plan.sizePerChunk;
+  w.chunkSize = p.plan.chunkSize;
+  w.minChunk = p.plan.minChunk;
+  w.nBlocks = (int16_t)da.nBlocks;
+  w.refNthreads = (int16_t)p.plan.refNthreads;
+  w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
+  w.workIndex = comm->workIndex++;
+  // flag reset when workIndex approaches overflow (enqueue.cc:714-721)
+  if (comm->flagsNeedReset || comm->workIndex > 0xFFFFFFFFu - 4096u) comm->flagsNeedReset = true;
+  return w;
+}
+
+ncclResult_t launchGroup(std::vector<Planned*>& ps) {
+  ncclComm* c0 = ps[0]->op.comm;
+  int dev = c0->cudaDev;
+  hipStream_t primary = ps[0]->op.stream;
+  LaunchArgs args;
+  memset(&args, 0, sizeof(args));
+  int blocks = 0;
+  std::vector<ncclComm*> resets;
+  for (size_t i = 0; i < ps.size(); i++) {
+    RankWork w = makeWork(*ps[i]);
+    w.blockBase = (int16_t)blocks;
+    blocks += w.nBlocks;
+    args.w[i] = w;
+    if (ps[i]->op.comm->flagsNeedReset) resets.push_back(ps[i]->op.comm);
+  }
+  args.nRanks = (int)ps.size();
+  if (blocks == 0) return ncclSuccess;
+  EventPool& pool = tEvents[dev];
+  pool.used = 0;
+  for (size_t i = 1; i < ps.size(); i++) {
+    if (ps[i]->op.stream != primary) {
+      hipEvent_t e = pool.get();
+      hipEventRecord(e, ps[i]->op.stream);
+      hipStreamWaitEvent(primary, e, 0);
+    }
+  }
+  for (ncclComm* c : resets) {
+    hipMemsetAsync(c->dFlags, 0, (size_t)kFlagSlots * kFlagStride * sizeof(uint64_t), primary);
+    c->workIndex = 1;
+    c->flagsNeedReset = false;
+  }
+  const Planned& p0 = *ps[0];
+  LaunchFn fn = getLaunchFn(p0.plan.dtype, p0.op.op, p0.plan.proto);
+  if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, (int)p0.op.op, p0.plan.proto); return ncclInvalidArgument; }
+  if (fn(args, blocks, (void*)primary) != 0) {
+    WARN("MSCCL: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
+    return ncclUnhandledCudaError;
+  }
+  for (size_t i = 1; i < ps.size(); i++) {
+    if (ps[i]->op.stream != primary) {
+      hipEvent_t e = pool.get();
+      hipEventRecord(e, primary);
+      hipStreamWaitEvent(ps[i]->op.stream, e, 0);
+    }
+  }
+  return ncclSuccess;
+}
+
+}  // namespace
+
+bool groupActive() { return tGroupDepth > 0; }
+void groupAddInit(std::function<ncclResult_t()> fn, ncclComm* comm) { tInits.emplace_back(std::move(fn), comm); }
+void groupAddOp(const CollOp& op) { tOps.push_back(op); }
+
+ncclResult_t executeOps(std::vector<CollOp>& ops) {
+  // rounds: the k-th op of every communicator runs in round k
+  std::vector<ncclComm*> order;
+  std::map<ncclComm*, std::vector<size_t>> perComm;
+  for (size_t i = 0; i < ops.size(); i++) {
+    if (!perComm.count(ops[i].comm)) order.push_back(ops[i].comm);
+    perComm[ops[i].comm].push_back(i);
+  }
+  size_t rounds = 0;
+  for (auto& kv : perComm) rounds = std::max(rounds, kv.second.size());
+  int saved = 0;
+  hipGetDevice(&saved);
+  ncclResult_t res = ncclSuccess;
+  for (size_t k = 0; k < rounds && res == ncclSuccess; k++) {
+    std::vector<Planned> planned;
+    planned.reserve(order.size());
+    for (ncclComm* c : order) {
+      auto& v = perComm[c];
+      if (k >= v.size()) continue;
+      Planned p;
+      res = planOp(ops[v[k]], &p);
+      if (res != ncclSuccess) break;
+      planned.push_back(p);
+    }
+    if (res != ncclSuccess) break;
+    // copies / no-ops
+    std::map<std::tuple<int, int, int, int>, std::vector<Planned*>> launches;
+    for (auto& p : planned) {
+      if (p.noop) continue;
+      hipSetDevice(p.op.comm->cudaDev);
+      if (p.memcpyOnly) {
+        if (hipMemcpyAsync(p.op.recvbuff, p.op.sendbuff, p.copyBytes, hipMemcpyDeviceToDevice, p.op.stream) != hipSuccess) {
+          res = ncclUnhandledCudaError;
+          break;
+        }
+        continue;
+      }
+      launches[std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, (int)p.op.op, p.plan.proto)].push_back(&p);
+    }
+    for (auto& kv : launches) {
+      if (res != ncclSuccess) break;
+      auto& list = kv.second;
+      hipSetDevice(std::get<0>(kv.first));
+      for (size_t s = 0; s < list.size() && res == ncclSuccess; s += kMaxLaunchRanks) {
+        if (list.size() > (size_t)kMaxLaunchRanks)
+          WARN("MSCCL: %zu co-resident ranks on device %d exceed one launch (%d); launching in parts",
+               list.size(), std::get<0>(kv.first), kMaxLaunchRanks);
+        std::vector<Planned*> part(list.begin() + s, list.begin() + std::min(list.size(), s + kMaxLaunchRanks));
+        res = launchGroup(part);
+      }
+    }
+  }
+  hipSetDevice(saved);
+  return res;
+}
+
+}  // namespace msccl
+
+using namespace msccl;
+
+namespace {
+
+ncclResult_t enqueue(ncclComm* comm, int coll, const void* sendbuff, void* recvbuff, size_t count,
+                     ncclDataType_t dtype, ncclRedOp_t op, hipStream_t stream, int customAlgo, const char* name) {
+  if (!commValid(comm)) { WARN("%s : invalid communicator", name); return ncclInvalidArgument; }
+  if ((int)dtype < 0 || (int)dtype >= ncclNumTypes) { WARN("%s : invalid type %d", name, (int)dtype); return ncclInvalidArgument; }
+  if ((int)op < 0 || (int)op > (int)ncclMaxRedOp) { WARN("%s : invalid reduction operation %d", name, (int)op); return ncclInvalidArgument; }
+  if ((int)op >= (int)ncclNumOps) { WARN("%s : reduction operation %d unknown to this communicator", name, (int)op); return ncclInvalidArgument; }
+  if (count > 0 && (sendbuff == nullptr || recvbuff == nullptr)) { WARN("%s : buffer argument is NULL", name); return ncclInvalidArgument; }
+  CollOp o{comm, coll, sendbuff, recvbuff, count, dtype, op, stream, customAlgo};
+  if (groupActive()) {
+    groupAddOp(o);
+    return ncclSuccess;
+  }
+  std::vector<CollOp> v{o};
+  return executeOps(v);
+}
+
+}  // namespace
+
+extern "C" {
+
+ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                           ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+  return enqueue(comm, kAllReduce, sendbuff, recvbuff, count, datatype, op, stream, -1, "AllReduce");
+}
+
+ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recvcount, ncclDataType_t datatype,
+                               ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+  return enqueue(comm, kReduceScatter, sendbuff, recvbuff, recvcount, datatype, op, stream, -1, "ReduceScatter");
+}
+
+ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount, ncclDataType_t datatype,
+                           ncclComm_t comm, hipStream_t stream) {
+  return enqueue(comm, kAllGather, sendbuff, recvbuff, sendcount, datatype, ncclSum, stream, -1, "AllGather");
+}
+
+ncclResult_t ncclAllToAll(const void* sendbuff, void* recvbuff, size_t sendcount, ncclDataType_t datatype,
+                          ncclComm_t comm, hipStream_t stream) {
+  return enqueue(comm, kAllToAll, sendbuff, recvbuff, sendcount, datatype, ncclSum, stream, -1, "AllToAll");
+}
+
+ncclResult_t ncclCustomCollective(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                  int mscclAlgorithmIndex, ncclComm_t comm, hipStream_t stream) {
+  return enqueue(comm, kCustom, sendbuff, recvbuff, count, datatype, ncclSum, stream, mscclAlgorithmIndex,
+                 "CustomCollective");
+}
+
+ncclResult_t ncclGroupStart() {
+  if (tGroupDepth == 0) tGroupError = ncclSuccess;
+  tGroupDepth++;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGroupEnd() {
+  if (tGroupDepth == 0) { WARN("ncclGroupEnd: not in a group call."); return ncclInvalidUsage; }
+  if (--tGroupDepth > 0) return ncclSuccess;
+  ncclResult_t res = ncclSuccess;
+  if (!tInits.empty()) {
+    auto inits = std::move(tInits);
+    tInits.clear();
+    std::vector<ncclResult_t> rs(inits.size(), ncclSuccess);
+    std::vector<std::thread> th;
+    int dev = 0;
+    hipGetDevice(&dev);
+    for (size_t i = 0; i < inits.size(); i++)
+      th.emplace_back([&, i]() {
+        hipSetDevice(inits[i].second->cudaDev);
+        rs[i] = inits[i].first();
+      });
+    for (auto& t : th) t.join();
+    hipSetDevice(dev);
+    for (auto r : rs)
+      if (r != ncclSuccess) res = r;
+  }
+  if (!tOps.empty()) {
+    auto ops = std::move(tOps);
+    tOps.clear();
+    ncclResult_t r = executeOps(ops);
+    if (r != ncclSuccess) res = r;
+  }
+  return res;
+}
+
+}  // extern "C"

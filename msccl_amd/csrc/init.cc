@@ -1,0 +1,356 @@
+// Communicator creation / destruction (reference init.cc:87-1255, single-node MSCCL subset).
+#include <hip/hip_runtime.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include <mutex>
+#include <thread>
+
+#include "bootstrap.h"
+#include "comm.h"
+#include "debug.h"
+#include "group.h"
+
+using namespace msccl;
+
+namespace msccl {
+
+bool commValid(const ncclComm* comm) { return comm != nullptr && comm->magic == kCommMagic; }
+
+namespace {
+
+ncclResult_t hipErr(hipError_t e, const char* what) {
+  if (e == hipSuccess) return ncclSuccess;
+  WARN("%s failed: %s", what, hipGetErrorString(e));
+  return ncclUnhandledCudaError;
+}
+
+// Load MSCCL_XML_FILES / MSCCL_CONFIG for this rank (init.cc:781-800).
+ncclResult_t loadAlgos(ncclComm* comm) {
+  const char* files = getenv("MSCCL_XML_FILES");
+  const char* cfg = getenv("MSCCL_CONFIG");
+  if (files) loadAlgosFromXmlFiles(files, &comm->algos, kMaxChannels, comm->rank, comm->nRanks);
+  if (cfg) NCCLCHECK(loadAlgosFromConfig(cfg, &comm->algos, &comm->regs, kMaxChannels, comm->rank, comm->nRanks));
+  return ncclSuccess;
+}
+
+// Per-rank device state that does not depend on peers.
+ncclResult_t commLocalSetup(ncclComm* comm) {
+  NCCLCHECK(hipErr(hipSetDevice(comm->cudaDev), "hipSetDevice"));
+  if (comm->nRanks > 1) NCCLCHECK(loadAlgos(comm));
+  comm->timeoutSec = (double)envInt("MSCCL_AMD_TIMEOUT_SEC", 60);
+  NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+  NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostErr, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+  *comm->hostAbort = 0;
+  *comm->hostErr = 0;
+  NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devAbort, comm->hostAbort, 0), "hipHostGetDevicePointer"));
+  NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devErr, comm->hostErr, 0), "hipHostGetDevicePointer"));
+  NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, (size_t)kFlagSlots * kFlagStride * sizeof(uint64_t)), "hipMalloc flags"));
+  NCCLCHECK(hipErr(hipMemset(comm->dFlags, 0, (size_t)kFlagSlots * kFlagStride * sizeof(uint64_t)), "hipMemset"));
+  comm->workIndex = 1;  // flags start at 0 (init.cc:300-302)
+  NCCLCHECK(hipErr(hipEventCreateWithFlags(&comm->doneEvent, hipEventDisableTiming), "hipEventCreate"));
+  // scratch = max over algorithms of maxBytes * s_chunks / nchunksperloop (init.cc:809-835)
+  size_t scratch = 0;
+  for (auto& a : comm->algos)
+    if (a.nchunksPerLoop > 0) {
+      double need = (double)a.maxBytes * (double)a.nScratchChunks / (double)a.nchunksPerLoop;
+      size_t s = need > 1.8e19 ? (size_t)-1 : (size_t)need;
+      scratch = std::max(scratch, s);
+    }
+  size_t cap = (size_t)envInt("MSCCL_AMD_MAX_SCRATCH", (int64_t)8 << 30);
+  if (scratch > cap) {
+    INFO(kSubInit, "MSCCL scratch %zu bytes capped to %zu (MSCCL_AMD_MAX_SCRATCH)", scratch, cap);
+    scratch = cap;
+  }
+  if (scratch > 0) {
+    NCCLCHECK(hipErr(hipMalloc(&comm->scratch, scratch), "hipMalloc scratch"));
+    NCCLCHECK(hipErr(hipMemset(comm->scratch, 0, scratch), "hipMemset scratch"));
+    comm->scratchSize = scratch;
+  }
+  if (comm->nRanks > 1) NCCLCHECK(transportPlan(comm));
+  return ncclSuccess;
+}
+
+ncclResult_t commFinish(ncclComm* comm) {
+  NCCLCHECK(algoUpload(comm));
+  DevComm dc;
+  memset(&dc, 0, sizeof(dc));
+  dc.send = comm->dSend;
+  dc.recv = comm->dRecv;
+  dc.flags = comm->dFlags;
+  dc.abortFlag = comm->devAbort;
+  dc.errWord = comm->devErr;
+  dc.timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
+  NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
+  NCCLCHECK(hipErr(hipMemcpy(comm->dComm, &dc, sizeof(dc), hipMemcpyHostToDevice), "hipMemcpy"));
+  NCCLCHECK(hipErr(hipDeviceSynchronize(), "hipDeviceSynchronize"));
+  int nValid = 0;
+  for (auto& a : comm->algos) nValid += a.valid;
+  if (nValid) INFO(kSubInit, "Connected %d MSCCL algorithms", nValid);  // init.cc:841
+  return ncclSuccess;
+}
+
+struct RankRecord {
+  int32_t pid, dev;
+  uint64_t arenaPtr;
+  hipIpcMemHandle_t handle;
+};
+
+ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
+  SocketBootstrap* sb = nullptr;
+  NCCLCHECK(SocketBootstrap::connect(id, comm->rank, comm->nRanks, &sb));
+  comm->boot = sb;
+  comm->ownsBoot = true;
+  NCCLCHECK(commLocalSetup(comm));
+  const int n = comm->nRanks;
+  if (n > 1) {
+    RankRecord rec;
+    memset(&rec, 0, sizeof(rec));
+    rec.pid = getpid();
+    rec.dev = comm->cudaDev;
+    rec.arenaPtr = (uint64_t)comm->arena;
+    NCCLCHECK(hipErr(hipIpcGetMemHandle(&rec.handle, comm->arena), "hipIpcGetMemHandle"));
+    std::vector<char> all;
+    NCCLCHECK(sb->allgather(&rec, sizeof(rec), &all));
+    size_t tbytes = comm->table.size() * sizeof(PeerOffsets);
+    std::vector<char> tall;
+    NCCLCHECK(sb->allgather(comm->table.data(), tbytes, &tall));
+    std::vector<std::vector<PeerOffsets>> tables(n);
+    comm->peerArena.assign(n, nullptr);
+    comm->peerArenaIpc.assign(n, false);
+    for (int r = 0; r < n; r++) {
+      tables[r].resize(comm->table.size());
+      memcpy(tables[r].data(), tall.data() + (size_t)r * tbytes, tbytes);
+      RankRecord pr;
+      memcpy(&pr, all.data() + (size_t)r * sizeof(RankRecord), sizeof(pr));
+      if (r == comm->rank) {
+        comm->peerArena[r] = comm->arena;
+      } else if (pr.pid == rec.pid) {
+        if (pr.dev != comm->cudaDev) {
+          hipError_t e = hipDeviceEnablePeerAccess(pr.dev, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hipErr(e, "hipDeviceEnablePeerAccess");
+          (void)hipGetLastError();
+        }
+        comm->peerArena[r] = (char*)pr.arenaPtr;
+      } else {
+        void* p = nullptr;
+        NCCLCHECK(hipErr(hipIpcOpenMemHandle(&p, pr.handle, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle"));
+        comm->peerArena[r] = (char*)p;
+        comm->peerArenaIpc[r] = true;
+      }
+    }
+    NCCLCHECK(transportConnect(comm, tables, comm->peerArena));
+  }
+  NCCLCHECK(commFinish(comm));
+  NCCLCHECK(sb->barrier());
+  return ncclSuccess;
+}
+
+}  // namespace
+
+ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
+  if (!comm) return ncclSuccess;
+  hipSetDevice(comm->cudaDev);
+  hipDeviceSynchronize();
+  for (auto& d : comm->devAlgos) {
+    if (d.dTbs) hipFree(d.dTbs);
+    if (d.dBlob) hipFree(d.dBlob);
+  }
+  for (size_t r = 0; r < comm->peerArena.size(); r++)
+    if (comm->peerArenaIpc[r] && comm->peerArena[r]) hipIpcCloseMemHandle(comm->peerArena[r]);
+  if (comm->dSend) hipFree(comm->dSend);
+  if (comm->dRecv) hipFree(comm->dRecv);
+  if (comm->dComm) hipFree(comm->dComm);
+  if (comm->dFlags) hipFree(comm->dFlags);
+  if (comm->scratch) hipFree(comm->scratch);
+  if (comm->boot && comm->ownsBoot) {
+    if (peerBarrier) comm->boot->barrier();  // peers may still read our arena until everyone is done
+    delete comm->boot;
+  }
+  if (comm->arena) hipFree(comm->arena);
+  if (comm->hostAbort) hipHostFree(comm->hostAbort);
+  if (comm->hostErr) hipHostFree(comm->hostErr);
+  if (comm->doneEvent) hipEventDestroy(comm->doneEvent);
+  comm->magic = 0;  // commPoison (init.cc:108-110)
+  delete comm;
+  return ncclSuccess;
+}
+
+}  // namespace msccl
+
+extern "C" {
+
+ncclResult_t ncclGetVersion(int* version) {
+  if (!version) return ncclInvalidArgument;
+  *version = NCCL_VERSION_CODE;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclGetUniqueId(ncclUniqueId* out) {
+  if (!out) { WARN("ncclGetUniqueId : uniqueId argument is NULL"); return ncclInvalidArgument; }
+  return bootstrapCreateRoot(out);
+}
+
+ncclResult_t ncclCommInitRank(ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
+  if (!newcomm) { WARN("ncclCommInitRank : comm argument is NULL"); return ncclInvalidArgument; }
+  if (nranks < 1 || myrank < 0 || myrank >= nranks) {
+    WARN("Invalid rank requested : %d/%d", myrank, nranks);
+    return ncclInvalidArgument;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return ncclUnhandledCudaError;
+  ncclComm* comm = new ncclComm();
+  comm->rank = myrank;
+  comm->nRanks = nranks;
+  comm->cudaDev = dev;
+  *newcomm = comm;
+  if (groupActive()) {
+    // ncclGroupStart/End around InitRank: run all inits in parallel at group end (group.cc:165-187)
+    groupAddInit([comm, commId]() { return initRankSync(comm, commId); }, comm);
+    return ncclSuccess;
+  }
+  ncclResult_t r = initRankSync(comm, commId);
+  if (r != ncclSuccess) {
+    commFree(comm, false);
+    *newcomm = nullptr;
+  }
+  return r;
+}
+
+// Single process, ndev ranks (init.cc:1099-1117).  devlist may repeat a device: such ranks are
+// co-resident on one GPU and a group of their calls becomes one fused launch.
+ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
+  if (!comms) { WARN("ncclCommInitAll : comms argument is NULL"); return ncclInvalidArgument; }
+  if (ndev < 1) { WARN("ncclCommInitAll : invalid ndev %d", ndev); return ncclInvalidArgument; }
+  int ndevices = 0;
+  if (hipGetDeviceCount(&ndevices) != hipSuccess) return ncclUnhandledCudaError;
+  int saved = 0;
+  hipGetDevice(&saved);
+  std::vector<ncclComm*> cs(ndev);
+  ncclResult_t res = ncclSuccess;
+  for (int i = 0; i < ndev && res == ncclSuccess; i++) {
+    int dev = devlist ? devlist[i] : i;
+    if (dev < 0 || dev >= ndevices) {
+      WARN("ncclCommInitAll : invalid device %d", dev);
+      res = ncclInvalidArgument;
+      break;
+    }
+    ncclComm* c = new ncclComm();
+    c->rank = i;
+    c->nRanks = ndev;
+    c->cudaDev = dev;
+    cs[i] = c;
+    res = commLocalSetup(c);
+  }
+  if (res == ncclSuccess && ndev > 1) {
+    std::vector<std::vector<PeerOffsets>> tables(ndev);
+    std::vector<char*> bases(ndev);
+    for (int i = 0; i < ndev; i++) {
+      tables[i] = cs[i]->table;
+      bases[i] = cs[i]->arena;
+    }
+    for (int i = 0; i < ndev && res == ncclSuccess; i++) {
+      hipSetDevice(cs[i]->cudaDev);
+      for (int j = 0; j < ndev; j++) {
+        if (cs[j]->cudaDev != cs[i]->cudaDev) {
+          hipError_t e = hipDeviceEnablePeerAccess(cs[j]->cudaDev, 0);
+          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+            WARN("hipDeviceEnablePeerAccess(%d -> %d) failed: %s", cs[i]->cudaDev, cs[j]->cudaDev, hipGetErrorString(e));
+            res = ncclUnhandledCudaError;
+          }
+          (void)hipGetLastError();
+        }
+      }
+      cs[i]->peerArena = bases;
+      cs[i]->peerArenaIpc.assign(ndev, false);
+      if (res == ncclSuccess) res = transportConnect(cs[i], tables, bases);
+    }
+  }
+  for (int i = 0; i < ndev && res == ncclSuccess; i++) {
+    hipSetDevice(cs[i]->cudaDev);
+    res = commFinish(cs[i]);
+  }
+  hipSetDevice(saved);
+  if (res != ncclSuccess) {
+    for (auto* c : cs)
+      if (c) commFree(c, false);
+    return res;
+  }
+  for (int i = 0; i < ndev; i++) comms[i] = cs[i];
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;
+  if (!commValid(comm)) { WARN("comm %p has already been destroyed", (void*)comm); return ncclInvalidArgument; }
+  int saved = 0;
+  hipGetDevice(&saved);
+  ncclResult_t r = commFree(comm, true);
+  hipSetDevice(saved);
+  return r;
+}
+
+ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;
+  if (!commValid(comm)) return ncclInvalidArgument;
+  __atomic_store_n(comm->hostAbort, 1u, __ATOMIC_SEQ_CST);  // kernels poll it in every spin (init.cc:1197)
+  int saved = 0;
+  hipGetDevice(&saved);
+  ncclResult_t r = commFree(comm, false);
+  hipSetDevice(saved);
+  return r;
+}
+
+const char* ncclGetErrorString(ncclResult_t code) {
+  switch (code) {
+    case ncclSuccess: return "no error";
+    case ncclUnhandledCudaError: return "unhandled cuda error";
+    case ncclSystemError: return "unhandled system error";
+    case ncclInternalError: return "internal error";
+    case ncclInvalidArgument: return "invalid argument";
+    case ncclInvalidUsage: return "invalid usage";
+    default: return "unknown result code";
+  }
+}
+
+ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
+  if (!commValid(comm) || !asyncError) return ncclInvalidArgument;
+  uint32_t e = __atomic_load_n(comm->hostErr, __ATOMIC_SEQ_CST);
+  if (e == kDevTimeout) comm->asyncError = ncclSystemError;
+  else if (e == kDevAbort) comm->asyncError = ncclSystemError;
+  else if (e != 0) comm->asyncError = ncclInternalError;
+  *asyncError = comm->asyncError;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  if (!commValid(comm) || !count) return ncclInvalidArgument;
+  *count = comm->nRanks;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* devid) {
+  if (!commValid(comm) || !devid) return ncclInvalidArgument;
+  *devid = comm->cudaDev;
+  return ncclSuccess;
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  if (!commValid(comm) || !rank) return ncclInvalidArgument;
+  *rank = comm->rank;
+  return ncclSuccess;
+}
+
+const char* ncclGetLastError(ncclComm_t comm) { return lastError(); }
+
+ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,
+                                      ncclScalarResidence_t residence, ncclComm_t comm) {
+  WARN("ncclRedOpCreatePreMulSum: PreMulSum is not an MSCCL-eligible operator (tuning.cc:345) and the "
+       "ring/tree fallback is not built");
+  return ncclInvalidUsage;
+}
+
+ncclResult_t ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm) { return ncclInvalidArgument; }
+
+}  // extern "C"

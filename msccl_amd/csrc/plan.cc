@@ -1,0 +1,174 @@
+#include "plan.h"
+
+#include <stdlib.h>
+#include <string.h>
+#include <strings.h>
+
+#include <algorithm>
+#include <string>
+
+#include "debug.h"
+#include "device/devcomm.h"
+
+namespace msccl {
+
+int refTypeSize(int t) {  // core.h:33-53
+  switch (t) {
+    case 0: case 1: return 1;
+    case 6: case 9: return 2;
+    case 2: case 3: case 7: return 4;
+    case 4: case 5: case 8: return 8;
+    default: return -1;
+  }
+}
+
+bool inPlaceOf(int coll, const void* send, const void* recv, size_t count, int dtype, int rank) {
+  const char* s = (const char*)send;
+  const char* r = (const char*)recv;
+  size_t ts = (size_t)refTypeSize(dtype);
+  if (coll == kAllGather) return s == r + (size_t)rank * count * ts;
+  if (coll == kReduceScatter) return r == s + (size_t)rank * count * ts;
+  return s == r;
+}
+
+// parseList (tuning.cc:34-55): "^A,B" disables, "A,B" enables only those
+static bool listEnables(const char* str, const char* name, bool def) {
+  if (!str) return def;
+  bool invert = str[0] == '^';
+  std::string s(str + (invert ? 1 : 0));
+  bool found = false;
+  size_t p = 0;
+  while (p <= s.size()) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    if (!strcasecmp(s.substr(p, q - p).c_str(), name)) found = true;
+    p = q + 1;
+  }
+  return invert ? !found : found;
+}
+
+bool mscclEnabled() {
+  // The reference needs NCCL_ALGO to contain MSCCL for AllReduce (tuning.cc:186,217) because
+  // ring/tree exist next to it; here MSCCL is the only algorithm, so it is on unless excluded.
+  return listEnables(getenv("NCCL_ALGO"), "MSCCL", true);
+}
+
+bool protoEnabled(int proto) {
+  static const char* names[3] = {"LL", "LL128", "Simple"};
+  return listEnables(getenv("NCCL_PROTO"), names[proto], true);
+}
+
+static void argsCheck(const CallDesc& c, int64_t* count, int* dtype, int64_t* nBytes) {
+  *nBytes = (int64_t)c.count * refTypeSize(c.dtype);
+  *count = (int64_t)c.count;
+  *dtype = c.dtype;
+  if (c.coll == kAllGather || c.coll == kBroadcast || c.coll == kAllToAll) {
+    *count = *nBytes;
+    *dtype = 0;
+  }
+  if (c.coll == kAllGather || c.coll == kReduceScatter || c.coll == kAllToAll) *nBytes *= c.nRanks;
+}
+
+int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c) {
+  if (!(c.redop == 0 || c.redop == 1 || c.redop == 2 || c.redop == 3)) return -1;  // tuning.cc:345
+  if (!mscclEnabled()) return -1;
+  int64_t count, nBytes;
+  int dt;
+  argsCheck(c, &count, &dt, &nBytes);
+  int64_t total = (c.coll == kAllToAll || c.coll == kAllGather || c.coll == kReduceScatter) ? count * c.nRanks : count;
+  auto ok = [&](const Algorithm& a) {
+    return a.valid && protoEnabled(a.proto) && a.coll == c.coll && a.inPlace == (int)c.inPlace &&
+           a.ngpus == c.nRanks && a.nchunksPerLoop > 0 && total % a.nchunksPerLoop == 0;
+  };
+  if (c.customAlgo >= 0) {
+    if (c.customAlgo < (int)algos.size() && algos[c.customAlgo].valid && algos[c.customAlgo].coll == kCustom) return c.customAlgo;
+    return -1;
+  }
+  if (!regs.empty()) {  // MSCCL_CONFIG registrations (tuning.cc:350-363)
+    for (auto& r : regs) {
+      if (r.minBytes <= nBytes && (nBytes < r.maxBytes || r.maxBytes == -1)) {
+        if (r.algoIndex < (int)algos.size() && ok(algos[r.algoIndex]) && protoEnabled(r.proto)) return r.algoIndex;
+      }
+    }
+    return -1;
+  }
+  for (size_t i = 0; i < algos.size(); i++) {
+    const Algorithm& a = algos[i];
+    if (ok(a) && nBytes >= a.minBytes && nBytes < a.maxBytes) return (int)i;
+  }
+  return -1;
+}
+
+static int getNthreads(const char* env, int lo, int hi, int def) {  // tuning.cc:14-32
+  int64_t nt = envInt(env, -2);
+  if (nt > 0) {
+    if (nt % kRefWarp != 0) return hi;
+    if (nt > hi) return hi;
+    if (nt < lo) return lo;
+    return (int)nt;
+  }
+  return def;
+}
+
+int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, Plan* p) {
+  const Algorithm& a = algos[algoIndex];
+  *p = Plan();
+  p->algoIndex = algoIndex;
+  p->proto = protoOverride >= 0 ? protoOverride : a.proto;
+  argsCheck(c, &p->count, &p->dtype, &p->nBytes);
+  int nt;
+  if (p->proto == kProtoSimple) nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512);
+  else if (p->proto == kProtoLL) nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512);
+  else nt = getNthreads("NCCL_LL128_NTHREADS", 640 / 4, 640, 640);
+  if (a.nThreads > 0) nt = std::min(nt, a.nThreads);
+  if (p->proto == kProtoSimple) nt += kRefWarp;  // extra sync warp (enqueue.cc:516-517)
+  p->refNthreads = nt;
+  int64_t bs[3] = {envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16),
+                   envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8), envInt("NCCL_BUFFSIZE", 1 << 22)};
+  int64_t stepSize = bs[p->proto] / kFifoSteps;
+  int64_t chunkSteps = p->proto == kProtoSimple ? kChunkSteps : 1;
+  int64_t chunkSize = stepSize * chunkSteps;
+  int64_t chunkEff = chunkSize;
+  if (p->proto == kProtoLL) chunkEff /= 2;
+  if (p->proto == kProtoLL128) chunkEff = (chunkSize / 16) * 15;
+  p->nchunksPerLoop = a.nchunksPerLoop;
+  int ts = refTypeSize(p->dtype);
+  if (p->nBytes % a.nchunksPerLoop != 0) {
+    WARN("MSCCL: something went wrong. MSCCL algorithm needs the input buffer to be divisible by %d", a.nchunksPerLoop);
+    return 3;
+  }
+  if (p->proto == kProtoSimple && chunkSize % ((nt - kRefWarp) * 8 / ts) != 0) {
+    WARN("chunkSize (%ld) should be divisble by (nthreads-WARP_SIZE) (%d) for Simple protocol", (long)chunkSize, nt - kRefWarp);
+    return 3;
+  }
+  int64_t mac = 0;
+  if (p->nBytes > 0) {
+    int64_t perChunk = (p->nBytes + a.nchunksPerLoop - 1) / a.nchunksPerLoop;
+    mac = std::max<int64_t>(1, chunkEff / perChunk);
+  }
+  if (mac == 0) { WARN("MSCCL: something went wrong. Max allowed count is 0"); return 3; }
+  if (mac >= kMaxCount) mac = kMaxCount - 1;
+  p->maxAllowedCount = (int)mac;
+  p->sizeMultiplier = (c.coll == kReduceScatter || c.coll == kAllGather || c.coll == kAllToAll) ? c.nRanks : 1;
+  p->scratchNeeded = (size_t)p->nBytes * (size_t)a.nScratchChunks / (size_t)a.nchunksPerLoop;
+
+  // interpreter parameters (msccl_interpreter.h:79-86)
+  int64_t bytePerStep;
+  if (p->proto == kProtoLL) {
+    bytePerStep = bs[0] / kFifoSteps / 2;
+    p->minChunk = (int64_t)nt * (8 / ts);
+  } else if (p->proto == kProtoLL128) {
+    bytePerStep = (bs[1] / kFifoSteps) * 15 / 16;
+    p->minChunk = (int64_t)nt * ((8 * 15 * 8 / 16) / ts) / 2;
+  } else {
+    bytePerStep = bs[2] / kFifoSteps;
+    p->minChunk = (int64_t)(nt - kRefWarp) * 8 / ts;
+  }
+  p->chunkSize = (int64_t)(int)(bytePerStep / ts * (p->proto == kProtoSimple ? kChunkSteps : 1));
+  p->sizePerChunk = (p->count * p->sizeMultiplier) / a.nchunksPerLoop;
+  p->nIters = p->chunkSize > 0 ? (int)((p->sizePerChunk + p->chunkSize - 1) / p->chunkSize) : 0;
+  if (p->minChunk <= 0) p->minChunk = 1;
+  return 0;
+}
+
+}  // namespace msccl

@@ -1,0 +1,56 @@
+// MSCCL algorithm selection + per-call chunk math (pure host functions, no GPU).
+//
+//   ArgsCheck                     misc/argcheck.cc:36-80
+//   in-place / totalCount         graph/tuning.cc:312-342
+//   algorithm match               graph/tuning.cc:344-382 (+ NCCL_ALGO / NCCL_PROTO gates, 185-218)
+//   thread counts                 graph/tuning.cc:14-32,78-85; enqueue.cc:486-523
+//   chunk math / maxAllowedCount  enqueue.cc:591-734; scratch check enqueue.cc:580-589
+//   interpreter chunk parameters  collectives/device/msccl_interpreter.h:79-113
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "algo.h"
+
+namespace msccl {
+
+struct CallDesc {
+  int coll;          // Coll
+  size_t count;      // user count (recvcount for RS, sendcount for AG)
+  int dtype;         // ncclDataType_t
+  int redop;         // ncclRedOp_t
+  int nRanks, rank;
+  bool inPlace;
+  int customAlgo = -1;  // ncclCustomCollective algorithm index
+};
+
+struct Plan {
+  int algoIndex = -1;
+  int proto = 0;
+  int refNthreads = 0;
+  int64_t count = 0;        // interpreter count (bytes for AllGather/AllToAll)
+  int dtype = 0;            // interpreter element type
+  int sizeMultiplier = 1;
+  int64_t nBytes = 0;
+  int maxAllowedCount = 0;
+  int nchunksPerLoop = 0;
+  int64_t sizePerChunk = 0; // elements per MSCCL chunk
+  int64_t chunkSize = 0;    // elements per interpreter iteration
+  int64_t minChunk = 0;     // LL: nthreads*8/ts; Simple: (nthreads-32)*8/ts
+  size_t scratchNeeded = 0;
+  int nIters = 0;
+};
+
+int refTypeSize(int dtype);
+bool inPlaceOf(int coll, const void* send, const void* recv, size_t count, int dtype, int rank);
+// Returns the selected algorithm index or -1 (the reference falls back to ring/tree there).
+int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c);
+// Fills *p; returns an ncclResult_t code.
+int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, Plan* p);
+// NCCL_ALGO / NCCL_PROTO gates
+bool mscclEnabled();
+bool protoEnabled(int proto);
+
+}  // namespace msccl

@@ -1,0 +1,288 @@
+"""MSCCL XML schedule generators (the msccl-tools algorithms the benchmarks need).
+
+msccl-tools (the Python DSL that emits MSCCL XML) is not installed in this image, so the
+schedules used by the benchmarks and tests are generated here.  The output is the
+msccl-tools XML dialect the reference loader accepts (graph/topo.cc:759-1193): one <algo>
+with <gpu>/<tb>/<step> children, steps numbered densely from 0, `nop` steps carrying extra
+dependencies and chained `re` steps that the loader fuses into one multi-source reduction.
+
+allreduce_allpairs reproduces the structure of msccl-tools' "allreduce_pairs" as shipped by
+RCCL (/opt/rocm/share/rccl/msccl-algorithms/allreduce-allpairs-8n-ll-32tb.xml): for n ranks and
+I instances (channels) the loop has I*n*n chunks, rank r owns chunks [k*n*n + r*n, +n) of
+instance k; thread block (k, peer p) sends the peer's n chunks to the peer's scratch, receives the
+peer's copy of its own chunks, reduces owned chunk p from all scratch slots and then exchanges
+the reduced chunks; thread block k (one per instance) reduces owned chunk r.  For n=8, I=4 the
+generated file is step-for-step the shipped 32-tb schedule (checked in tests).
+"""
+from __future__ import annotations
+
+import io
+from typing import Dict, List, Optional, Tuple
+
+Step = Tuple[str, str, int, str, int, int, int, int, int]  # type, srcbuf, srcoff, dstbuf, dstoff, cnt, depid, deps, hasdep
+
+
+class _Tb:
+    def __init__(self, tid: int, send: int, recv: int, chan: int):
+        self.id, self.send, self.recv, self.chan = tid, send, recv, chan
+        self.steps: List[Step] = []
+
+    def add(self, typ, srcbuf="i", srcoff=-1, dstbuf="o", dstoff=-1, cnt=0, depid=-1, deps=-1, hasdep=0) -> int:
+        self.steps.append((typ, srcbuf, srcoff, dstbuf, dstoff, cnt, depid, deps, hasdep))
+        return len(self.steps) - 1
+
+    def nop(self, depid: int, deps: int) -> int:
+        return self.add("nop", "i", -1, "o", -1, 0, depid, deps, 0)
+
+
+def _emit(name: str, proto: str, nchannels: int, ncpl: int, ngpus: int, coll: str, inplace: bool,
+          gpus: Dict[int, Tuple[int, int, int, List[_Tb]]], min_bytes: Optional[int], max_bytes: Optional[int],
+          nthreads: Optional[int] = None) -> str:
+    o = io.StringIO()
+    attrs = ('name="%s" proto="%s" nchannels="%d" nchunksperloop="%d" ngpus="%d" coll="%s" inplace="%d" '
+             'outofplace="%d"' % (name, proto, nchannels, ncpl, ngpus, coll, int(inplace), int(not inplace)))
+    if min_bytes is not None:
+        attrs += ' minBytes="%d"' % min_bytes
+    if max_bytes is not None:
+        attrs += ' maxBytes="%d"' % max_bytes
+    if nthreads is not None:
+        attrs += ' nthreads="%d"' % nthreads
+    o.write("<algo %s>\n" % attrs)
+    for g in sorted(gpus):
+        ic, oc, sc, tbs = gpus[g]
+        o.write('  <gpu id="%d" i_chunks="%d" o_chunks="%d" s_chunks="%d">\n' % (g, ic, oc, sc))
+        for tb in sorted(tbs, key=lambda t: t.id):
+            o.write('    <tb id="%d" send="%d" recv="%d" chan="%d">\n' % (tb.id, tb.send, tb.recv, tb.chan))
+            for s, (typ, sb, so, db, do, cnt, di, ds, hd) in enumerate(tb.steps):
+                o.write('      <step s="%d" type="%s" srcbuf="%s" srcoff="%d" dstbuf="%s" dstoff="%d" cnt="%d" '
+                        'depid="%d" deps="%d" hasdep="%d"/>\n' % (s, typ, sb, so, db, do, cnt, di, ds, hd))
+            o.write("    </tb>\n")
+        o.write("  </gpu>\n")
+    o.write("</algo>\n")
+    return o.getvalue()
+
+
+def allreduce_allpairs(n: int, instances: int = 1, proto: str = "LL", inplace: bool = True,
+                       min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
+                       nthreads: Optional[int] = None, name: str = "allreduce_pairs") -> str:
+    """All-pairs AllReduce: reduce-scatter into scratch, local reduce, all-gather (n >= 2)."""
+    if n < 2:
+        raise ValueError("allpairs needs at least 2 ranks")
+    I = instances
+    ncpl = I * n * n
+    gpus = {}
+    for r in range(n):
+        peers = [p for p in range(n) if p != r]
+        slot = {p: i for i, p in enumerate(peers)}
+        red = {k: _Tb(k, -1, -1, k) for k in range(I)}
+        ptb = {}
+        for pi, p in enumerate(peers):
+            for k in range(I):
+                tid = I + pi * I + k
+                ptb[(k, p)] = _Tb(tid, p, p, k)
+        ob = "i" if inplace else "o"
+        # step indices that others depend on
+        recv_step: Dict[Tuple[int, int], int] = {}
+        red_last: Dict[Tuple[int, int], int] = {}
+        copy_step: Dict[int, int] = {}
+        # peer tbs, phase 1: send peer's chunks, receive peer's copy of mine into scratch
+        for k in range(I):
+            base = k * n * n
+            for p in peers:
+                tb = ptb[(k, p)]
+                tb.add("s", "i", base + p * n, "s", k * (n - 1) * n + _slot_of(r, p) * n, n)
+                recv_step[(k, p)] = tb.add("r", "i", base + r * n, "s", k * (n - 1) * n + slot[p] * n, n, hasdep=1)
+        # reduce thread blocks (owned chunk 0 of each instance)
+        for k in range(I):
+            base = k * n * n
+            tb = red[k]
+            if not inplace:
+                copy_step[k] = tb.add("cpy", "i", base + r * n, "o", base + r * n, n, hasdep=1)
+            others = [ptb[(k, p)].id for p in peers]
+            for dep in others[1:]:
+                tb.nop(dep, 1)
+            # the reduce tb reduces owned chunk j = r, peer tb (k, p) reduces owned chunk j = p
+            srcs = [k * (n - 1) * n + slot[p] * n + r for p in peers]
+            for i, so in enumerate(srcs):
+                last = i == len(srcs) - 1
+                if i == 0:
+                    red_last[(k, -1)] = tb.add("re", "s", so, ob, base + r * n + r, 1, others[0], 1, int(last))
+                else:
+                    red_last[(k, -1)] = tb.add("re", "s", so, ob, base + r * n + r, 1, -1, -1, int(last))
+        # peer tbs: reduce owned chunk j = 1 + peer index, then exchange
+        for k in range(I):
+            base = k * n * n
+            for pi, p in enumerate(peers):
+                tb = ptb[(k, p)]
+                j = p
+                others = [ptb[(k, q)].id for q in peers if q != p]
+                first_dep = None
+                if inplace:
+                    for dep in others[1:]:
+                        tb.nop(dep, recv_step[(k, p)])
+                    if others:
+                        first_dep = (others[0], recv_step[(k, p)])
+                else:
+                    # the reduction target o[...] is written by the reduce tb's copy
+                    for dep in others:
+                        tb.nop(dep, recv_step[(k, p)])
+                    first_dep = (red[k].id, copy_step[k])
+                srcs = [k * (n - 1) * n + slot[q] * n + j for q in peers]
+                for i, so in enumerate(srcs):
+                    last = i == len(srcs) - 1
+                    if i == 0 and first_dep is not None:
+                        idx = tb.add("re", "s", so, ob, base + r * n + j, 1, first_dep[0], first_dep[1], int(last))
+                    else:
+                        idx = tb.add("re", "s", so, ob, base + r * n + j, 1, -1, -1, int(last))
+                red_last[(k, p)] = idx
+        for k in range(I):
+            base = k * n * n
+            for p in peers:
+                tb = ptb[(k, p)]
+                for q in peers:
+                    if q != p:
+                        tb.nop(ptb[(k, q)].id, red_last[(k, q)])
+                tb.add("s", ob, base + r * n, ob, base + r * n, n, red[k].id, red_last[(k, -1)])
+                tb.add("r", ob, base + p * n, ob, base + p * n, n)
+        tbs = list(red.values()) + list(ptb.values())
+        gpus[r] = (ncpl, 0 if inplace else ncpl, I * (n - 1) * n, tbs)
+    if max_bytes is None:
+        max_bytes = 1 << 62
+    return _emit(name, proto, I, ncpl, n, "allreduce", inplace, gpus, min_bytes, max_bytes, nthreads)
+
+
+def _slot_of(r: int, p: int) -> int:
+    """scratch slot of sender r on receiver p: peers of p in ascending order, p skipped."""
+    return r if r < p else r - 1
+
+
+def allreduce_ring(n: int, channels: int = 1, proto: str = "Simple", inplace: bool = True,
+                   min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
+                   nthreads: Optional[int] = None, strides: Optional[List[int]] = None,
+                   name: str = "allreduce_ring") -> str:
+    """Ring AllReduce, one ring per channel: s, rrs x (n-2), rrcs, rcs x (n-2), r.
+
+    Channel c walks the Hamiltonian cycle i -> i + stride_c (mod n); with strides coprime to n
+    (1, 3, 5, 7 on 8 ranks) the channels use disjoint directed xGMI links.
+    """
+    if strides is None:
+        cands = [s for s in range(1, n) if _gcd(s, n) == 1]
+        strides = [cands[c % len(cands)] for c in range(channels)]
+    ncpl = channels * n
+    gpus = {}
+    ob = "i" if inplace else "o"
+    for r in range(n):
+        tbs = []
+        for c in range(channels):
+            st = strides[c]
+            ring = [(i * st) % n for i in range(n)]
+            pos = ring.index(r)
+            nxt = ring[(pos + 1) % n]
+            prv = ring[(pos - 1) % n]
+            tb = _Tb(c, nxt, prv, c)
+
+            def ch(i):  # chunk of ring position i in channel c
+                return c * n + (i % n)
+            if not inplace:
+                pass
+            tb.add("s", "i", ch(pos), ob, ch(pos), 1)
+            for t in range(1, n - 1):
+                tb.add("rrs", "i", ch(pos - t), ob, ch(pos - t), 1)
+            cdone = ch(pos + 1)
+            tb.add("rrcs", "i", cdone, ob, cdone, 1)
+            for t in range(1, n - 1):
+                tb.add("rcs", ob, ch(pos + 1 - t), ob, ch(pos + 1 - t), 1)
+            tb.add("r", ob, ch(pos + 2), ob, ch(pos + 2), 1)
+            tbs.append(tb)
+        gpus[r] = (ncpl, 0 if inplace else ncpl, 0, tbs)
+    if max_bytes is None:
+        max_bytes = 1 << 62
+    return _emit(name, proto, channels, ncpl, n, "allreduce", inplace, gpus, min_bytes, max_bytes, nthreads)
+
+
+def reduce_scatter_allpairs(n: int, instances: int = 1, proto: str = "Simple", inplace: bool = False,
+                            min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
+                            nthreads: Optional[int] = None, name: str = "reduce_scatter_pairs") -> str:
+    """All-pairs ReduceScatter.  Input = n blocks of I chunks (block p -> rank p), output = I chunks."""
+    I = instances
+    ncpl = n * I
+    gpus = {}
+    for r in range(n):
+        peers = [p for p in range(n) if p != r]
+        slot = {p: i for i, p in enumerate(peers)}
+        tbs = []
+        ptb = {}
+        tid = I
+        for p in peers:
+            for k in range(I):
+                ptb[(k, p)] = _Tb(tid, p, p, k)
+                tid += 1
+        recv_step = {}
+        for k in range(I):
+            for p in peers:
+                tb = ptb[(k, p)]
+                tb.add("s", "i", p * I + k, "s", k * (n - 1) + _slot_of(r, p), 1)
+                recv_step[(k, p)] = tb.add("r", "i", r * I + k, "s", k * (n - 1) + slot[p], 1, hasdep=1)
+        for k in range(I):
+            tb = _Tb(k, -1, -1, k)
+            # output chunk k starts as my own block (in-place: the output aliases input block r)
+            if not inplace:
+                tb.add("cpy", "i", r * I + k, "o", k, 1)
+            others = [ptb[(k, p)].id for p in peers]
+            for dep in others[1:]:
+                tb.nop(dep, recv_step[(k, peers[0])])
+            for i, p in enumerate(peers):
+                last = i == len(peers) - 1
+                so = k * (n - 1) + slot[p]
+                if i == 0:
+                    tb.add("re", "s", so, "o", k, 1, others[0], recv_step[(k, peers[0])], int(last))
+                else:
+                    tb.add("re", "s", so, "o", k, 1, -1, -1, int(last))
+            tbs.append(tb)
+        tbs += list(ptb.values())
+        gpus[r] = (ncpl, I, I * (n - 1), tbs)
+    if max_bytes is None:
+        max_bytes = 1 << 62
+    return _emit(name, proto, I, ncpl, n, "reduce_scatter", inplace, gpus, min_bytes, max_bytes, nthreads)
+
+
+def allgather_allpairs(n: int, instances: int = 1, proto: str = "Simple", inplace: bool = False,
+                       min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
+                       nthreads: Optional[int] = None, name: str = "allgather_pairs") -> str:
+    """All-pairs AllGather.  Input = I chunks, output = n blocks of I chunks (block p from rank p)."""
+    I = instances
+    ncpl = n * I
+    gpus = {}
+    for r in range(n):
+        peers = [p for p in range(n) if p != r]
+        tbs = []
+        tid = 0
+        if not inplace:
+            for k in range(I):
+                tb = _Tb(tid, -1, -1, k)
+                tb.add("cpy", "i", k, "o", r * I + k, 1)
+                tbs.append(tb)
+                tid += 1
+        for p in peers:
+            for k in range(I):
+                tb = _Tb(tid, p, p, k)
+                tid += 1
+                tb.add("s", "i", k, "o", r * I + k, 1)
+                tb.add("r", "i", k, "o", p * I + k, 1)
+                tbs.append(tb)
+        gpus[r] = (I, ncpl, 0, tbs)
+    if max_bytes is None:
+        max_bytes = 1 << 62
+    return _emit(name, proto, I, ncpl, n, "allgather", inplace, gpus, min_bytes, max_bytes, nthreads)
+
+
+def _gcd(a: int, b: int) -> int:
+    while b:
+        a, b = b, a % b
+    return a
+
+
+def write(path: str, text: str) -> str:
+    with open(path, "w") as f:
+        f.write(text)
+    return path

@@ -1,0 +1,145 @@
+"""Shared GPU parity harness: run one collective through the C-ABI on co-resident ranks and
+compare with the CPU oracle (oracle/sim.py) on identical seeded inputs.
+
+Ranks are created with ncclCommInitAll(devlist=[0]*n) so all of them live on cuda:0 and a
+group of their calls is one fused launch — the same kernels, FIFOs and flag protocol as the
+multi-GPU path, with local HBM in place of xGMI.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import numpy as np
+
+import msccl_amd as M
+from oracle import loader as L
+from oracle import numerics as N
+from oracle import plan as P
+from oracle import sim as S
+
+TORCH_DT = None
+
+
+def torch_dtype(dt: int):
+    import torch
+    return {0: torch.int8, 1: torch.uint8, 2: torch.int32, 3: torch.int32, 4: torch.int64, 5: torch.int64,
+            6: torch.float16, 7: torch.float32, 8: torch.float64, 9: torch.int16}[dt]
+
+
+def to_torch(a: np.ndarray, dev):
+    import torch
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    elif a.dtype == np.uint64:
+        a = a.view(np.int64)
+    elif a.dtype == np.uint16:
+        a = a.view(np.int16)
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def from_torch(t, np_dtype) -> np.ndarray:
+    a = t.cpu().numpy()
+    return a.view(np_dtype)
+
+
+def gen_inputs(n: int, count: int, dt: int, seed: int, mode: str = "uniform") -> List[np.ndarray]:
+    """Per-rank inputs: uniform[-1,1) (fp) / small ints, or 'exact' small integers."""
+    out = []
+    for r in range(n):
+        rng = np.random.default_rng(seed * 1000 + r)
+        kind = N.DTYPES[dt][2]
+        if kind == "int" or mode == "exact":
+            v = rng.integers(-4, 5, size=count)
+            if kind == "int" and N.storage(dt) in (np.uint8, np.uint32, np.uint64):
+                v = rng.integers(0, 9, size=count)
+            out.append(N.from_float(dt, v.astype(np.float64)) if kind != "int" else v.astype(N.storage(dt)))
+        else:
+            v = rng.uniform(-1.0, 1.0, size=count)
+            out.append(N.from_float(dt, v))
+    return out
+
+
+def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, op: int = 0,
+                   in_place: bool = True, seed: int = 1, mode: str = "uniform", iters: int = 1,
+                   tmpdir: str = "/tmp", extra_xmls: Optional[List[str]] = None):
+    """Returns (gpu_outputs, oracle_outputs) as lists of numpy arrays (interpreter element type)."""
+    import torch
+    path = os.path.join(tmpdir, "msccl_test_%d_%d.xml" % (os.getpid(), abs(hash(xml_text)) % 100000))
+    with open(path, "w") as f:
+        f.write(xml_text)
+    os.environ["MSCCL_XML_FILES"] = ":".join([path] + (extra_xmls or []))
+    dev = torch.device("cuda:0")
+    comms = M.Comm.init_all([0] * nranks)
+    try:
+        algos = [L.parse_xml(xml_text, r, nranks) for r in range(nranks)]
+        ts = N.type_size(dt)
+        if coll == L.ALLREDUCE:
+            in_n, out_n = count, count
+        elif coll == L.REDUCE_SCATTER:
+            in_n, out_n = count * nranks, count
+        else:  # allgather
+            in_n, out_n = count, count * nranks
+        ins = gen_inputs(nranks, in_n, dt, seed, mode)
+        # GPU
+        t_in = [to_torch(x, dev) for x in ins]
+        if in_place:
+            if coll == L.ALLREDUCE:
+                t_out = t_in
+                sends = [t.data_ptr() for t in t_in]
+                recvs = sends
+            elif coll == L.REDUCE_SCATTER:
+                t_out = [t[r * count:(r + 1) * count] for r, t in enumerate(t_in)]
+                sends = [t.data_ptr() for t in t_in]
+                recvs = [t.data_ptr() for t in t_out]
+            else:
+                t_out = [torch.zeros(out_n, dtype=t_in[0].dtype, device=dev) for _ in range(nranks)]
+                for r in range(nranks):
+                    t_out[r][r * count:(r + 1) * count] = t_in[r]
+                sends = [t_out[r][r * count:(r + 1) * count].data_ptr() for r in range(nranks)]
+                recvs = [t.data_ptr() for t in t_out]
+        else:
+            t_out = [torch.full((out_n,), 7, dtype=t_in[0].dtype, device=dev) for _ in range(nranks)]
+            sends = [t.data_ptr() for t in t_in]
+            recvs = [t.data_ptr() for t in t_out]
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream().cuda_stream
+        for _ in range(iters):
+            with M.group():
+                for r, c in enumerate(comms):
+                    if coll == L.ALLREDUCE:
+                        c.all_reduce(sends[r], recvs[r], count, dt, op, stream)
+                    elif coll == L.REDUCE_SCATTER:
+                        c.reduce_scatter(sends[r], recvs[r], count, dt, op, stream)
+                    else:
+                        c.all_gather(sends[r], recvs[r], count, dt, stream)
+        torch.cuda.synchronize()
+        for c in comms:
+            err = c.async_error()
+            if err != 0:
+                raise M.NcclError(err, "kernel (async error)")
+        gpu = [from_torch(t, N.storage(dt) if coll != L.ALLGATHER else N.storage(dt)) for t in t_out]
+    finally:
+        for c in comms:
+            c.destroy()
+    # oracle
+    call = P.Call(coll, count, dt, op, nranks, 0, in_place)
+    idx = P.select([algos[0]], call)
+    assert idx == 0, "oracle selection failed"
+    plan = P.make_plan([algos[0]], call, 0)
+    o_in = [x.copy() for x in ins]
+    if coll == L.ALLGATHER:
+        o_in = [x.view(np.int8) for x in o_in]
+        o_out = [np.zeros(out_n * ts, np.int8) for _ in range(nranks)]
+    elif in_place:
+        o_out = [None] * nranks
+    else:
+        o_out = [np.full(out_n, 7, N.storage(dt)) if N.DTYPES[dt][2] != "bf16" else np.full(out_n, 7, np.uint16)
+                 for _ in range(nranks)]
+    for _ in range(iters):
+        res, _ = S.run(algos, plan, o_in, o_out, coll, in_place)
+        if iters > 1 and coll == L.ALLREDUCE and in_place:
+            o_in = res
+    if coll == L.ALLGATHER:
+        res = [r.view(N.storage(dt)) for r in res]
+    return gpu, [np.asarray(r) for r in res], ins
