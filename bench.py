@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""AllReduce bus-bandwidth benchmark for the MI355X MSCCL runtime (nccl-tests all_reduce_perf style).
+
+Metric (BASELINE.json): AllReduce bus-BW GB/s, device-resident, 128 B - 32 MiB sweep, with
+busBW = (S / t) * 2(n-1)/n (nccl-tests convention used by the reference README:57).
+
+  python bench.py                      # N=1: config C2 = 2-rank all-pairs LL fp32 AllReduce, both
+                                       # ranks co-resident on cuda:0 (one fused launch per step)
+  torchrun --nproc-per-node N bench.py --gpus N   # one rank per GPU, all-pairs LL over xGMI
+                                       # (fp32; fp16 at N=8 = config C3)
+
+A "step" is one AllReduce of S bytes per rank on every rank.  `value` is the bus bandwidth at
+the largest size of the sweep (32 MiB); the whole sweep is in `sweep`.  Inputs are resident in
+HBM before the timed region.  rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import msccl_amd as M  # noqa: E402
+from msccl_amd import xmlgen  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+XGMI_LINK_GBS = 153.0          # task statement, per link (see DESIGN.md calibration note)
+SIZES = [128 << k for k in range(19)]  # 128 B .. 32 MiB
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--vranks", type=int, default=2, help="co-resident ranks at --gpus 1 (config C2: 2)")
+    ap.add_argument("--proto", default="LL")
+    ap.add_argument("--dtype", default=None)
+    ap.add_argument("--instances", type=int, default=0, help="all-pairs instances for large sizes (0 = auto)")
+    ap.add_argument("--sizes", default=None, help="comma list of bytes (default 128B..32MiB)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--e2e", action="store_true", help="also time H2D + AllReduce + D2H")
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args()
+
+
+def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int):
+    """Algorithmic HBM bytes and wire bytes of one launch for one rank (whole schedule)."""
+    f = 2 if proto in (0, 1) else 1  # LL: a 16-B line carries 8 B of data
+    hbm = wire = 0
+    for tb in algo["tbs"]:
+        for t in tb["transfers"]:
+            typ, cnt, nred = t[0], t[5], t[10]
+            b = cnt * size_per * ts
+            if typ == 0:      # s
+                hbm += b + f * b; wire += f * b
+            elif typ == 1:    # r
+                hbm += f * b + b
+            elif typ == 2:    # rcs
+                hbm += f * b + b + f * b; wire += f * b
+            elif typ == 3:    # rrs
+                hbm += f * b + b + f * b; wire += f * b
+            elif typ == 4:    # rrc
+                hbm += f * b + b + b
+            elif typ == 5:    # rrcs
+                hbm += f * b + b + b + f * b; wire += f * b
+            elif typ == 6:    # cpy
+                hbm += 2 * b
+            elif typ == 7:    # re
+                hbm += (nred + 1) * b + b
+    return hbm, wire
+
+
+def make_xmls(n: int, proto: str, inst_large: int, tmp: str):
+    """Small sizes: 1 instance (ncpl = n*n, smallest divisibility); large: inst_large instances."""
+    ncpl_small = n * n
+    thresh = 64 << 10
+    small = xmlgen.allreduce_allpairs(n, 1, proto, True, 0, thresh, name="allpairs_small")
+    large = xmlgen.allreduce_allpairs(n, inst_large, proto, True, thresh, (1 << 30) + 1, name="allpairs_large")
+    ps = os.path.join(tmp, "bench_ap%d_%s_small_%d.xml" % (n, proto, os.getpid()))
+    pl = os.path.join(tmp, "bench_ap%d_%s_i%d_%d.xml" % (n, proto, inst_large, os.getpid()))
+    open(ps, "w").write(small)
+    open(pl, "w").write(large)
+    return [ps, pl], ncpl_small, inst_large * n * n, thresh
+
+
+def cpu_baseline(n: int, nbytes: int, dt: int, seconds: float):
+    """Time oracle/cpu_allreduce.c (OpenMP) on a bounded sample: repeated n-rank AllReduces."""
+    libp = os.path.join(ROOT, "oracle", "build", "libcpu_allreduce.so")
+    if not os.path.exists(libp):
+        return None
+    lib = ctypes.CDLL(libp)
+    ts = M.TYPE_SIZE[dt]
+    cnt = nbytes // ts
+    bufs = [np.random.default_rng(r).standard_normal(cnt).astype(np.float32 if dt == M.FLOAT32 else np.float16)
+            if dt != M.BFLOAT16 else np.zeros(cnt, np.uint16) for r in range(n)]
+    ptrs = (ctypes.c_void_p * n)(*[b.ctypes.data for b in bufs])
+    chunk = max(1, cnt // (n * n))
+    threads = lib.cpu_allreduce_allpairs(ptrs, n, ctypes.c_long(cnt), ctypes.c_long(chunk), dt)
+    reps = 0
+    t0 = time.perf_counter()
+    while True:
+        lib.cpu_allreduce_allpairs(ptrs, n, ctypes.c_long(cnt), ctypes.c_long(chunk), dt)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    t = el / reps
+    bus = nbytes / t * 2 * (n - 1) / n / 1e9
+    return {"value": round(bus, 3), "unit": "GB/s", "cores": int(threads), "kind": "port",
+            "sample": "%d x %d-rank all-pairs-order AllReduce of %d B %s per rank (oracle/cpu_allreduce.c, "
+                      "OpenMP, %.1f s)" % (reps, n, nbytes, {7: "fp32", 6: "fp16", 9: "bf16"}[dt], el),
+            "ms_per_allreduce": round(t * 1e3, 4)}
+
+
+def main():
+    a = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    multi = world > 1
+    n = world if multi else a.vranks
+    dtname = a.dtype or ("fp16" if (multi and world >= 8) else "fp32")
+    dt = M.DTYPE_NAMES[dtname]
+    ts = M.TYPE_SIZE[dt]
+    proto_id = {"LL": 0, "LL128": 1, "Simple": 2}[a.proto]
+    inst = a.instances or (16 if n <= 2 else (8 if n <= 4 else 4))
+    sizes = [int(s) for s in a.sizes.split(",")] if a.sizes else SIZES
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    xmls, ncpl_small, ncpl_large, thresh = make_xmls(n, a.proto, inst, tmp)
+    os.environ["MSCCL_XML_FILES"] = ":".join(xmls)
+    os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "30")
+
+    if multi:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        obj = [M.get_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comms = [M.Comm.init_rank(world, obj[0], rank)]
+        devs = [torch.device("cuda", local)]
+        my_ranks = [rank]
+    else:
+        comms = M.Comm.init_all([0] * n)
+        devs = [torch.device("cuda", 0)] * n
+        my_ranks = list(range(n))
+
+    def barrier():
+        if multi:
+            torch.distributed.barrier()
+
+    stream = torch.cuda.current_stream(devs[0])
+    maxb = max(sizes)
+    bufs = [torch.empty(maxb // 4 + 64, dtype=torch.float32, device=d).uniform_(-1, 1) for d in devs]
+    algo_large = M.algo_json(xmls[1], my_ranks[0], n)
+    algo_small = M.algo_json(xmls[0], my_ranks[0], n)
+
+    def one_step(nbytes):
+        cnt = nbytes // ts
+        with M.group():
+            for c, b in zip(comms, bufs):
+                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+
+    results = []
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for nbytes in sizes:
+        cnt = nbytes // ts
+        ncpl = ncpl_small if nbytes < thresh else ncpl_large
+        if cnt % ncpl:
+            continue
+        for _ in range(a.warmup):
+            one_step(nbytes)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(a.steps):
+            one_step(nbytes)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        barrier()
+        wall = time.perf_counter() - t0
+        ev_ms = ev0.elapsed_time(ev1) / a.steps
+        t = wall / a.steps
+        if multi:
+            tt = torch.tensor([t, ev_ms], dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            t, ev_ms = float(tt[0]), float(tt[1])
+        for c in comms:
+            if c.async_error() != 0:
+                raise RuntimeError("kernel reported an error (timeout/abort) at %d bytes" % nbytes)
+        algbw = nbytes / t / 1e9
+        bus = algbw * 2 * (n - 1) / n
+        algo = algo_small if nbytes < thresh else algo_large
+        size_per = cnt // ncpl
+        hbm, wire = schedule_bytes(algo, size_per, ts, proto_id)
+        results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
+                         "algbw": round(algbw, 3), "busbw": round(bus, 3),
+                         "hbm_bytes_per_rank": hbm, "wire_bytes_per_rank": wire})
+        if not a.quiet and rank == 0:
+            print("# %10d B  %9.2f us  algbw %8.2f  busbw %8.2f GB/s" % (nbytes, t * 1e6, algbw, bus),
+                  file=sys.stderr, flush=True)
+    head = results[-1]
+    # roofline of the dominant (largest) launch
+    ranks_on_gpu = 1 if multi else n
+    kernel_s = head["kernel_ms"] / 1e3
+    achieved = head["hbm_bytes_per_rank"] * ranks_on_gpu / kernel_s / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "mscclKernel<%s,Sum,%s>" % (dtname, a.proto),
+            "algorithmic_bytes_per_launch": head["hbm_bytes_per_rank"] * ranks_on_gpu,
+            "kernel_ms": head["kernel_ms"]}
+    if multi:
+        link = XGMI_LINK_GBS * (n - 1)
+        roof["xgmi"] = {"busbw": head["busbw"], "peak": link, "frac": round(head["busbw"] / link, 4),
+                        "ll_ceiling": round(link * (0.5 if proto_id == 0 else 1.0), 1)}
+    e2e = None
+    if a.e2e and rank == 0 and not multi:
+        e2e = measure_e2e(comms, n, maxb, dt, ts, stream, devs[0])
+    cpu = None
+    if not a.no_cpu and rank == 0:
+        cpu = cpu_baseline(2 if not multi else n, maxb, dt if dt in (6, 7, 9) else 7, a.cpu_seconds)
+    out = {
+        "metric": "AllReduce bus-BW GB/s (device-resident), 128B-32MB",
+        "value": head["busbw"], "unit": "GB/s", "n_gpus": world if multi else 1, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": head["ms"], "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}.get(dtname, dtname),
+        "data": "synthetic",
+        "config": {"workload": ("C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
+                                "(fused launch, local HBM in place of xGMI)" % (n, a.proto, dtname)) if not multi
+                   else ("%s: %d-rank all-pairs %s AllReduce over xGMI, %s, one rank per GPU"
+                         % ("C3" if n == 8 else "C2-family", n, a.proto, dtname)),
+                   "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
+                   "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]]},
+        "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "sweep": [{k: r[k] for k in ("bytes", "ms", "busbw")} for r in results],
+    }
+    if e2e:
+        out["e2e"] = e2e
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    for c in comms:
+        c.destroy()
+    if multi:
+        torch.distributed.destroy_process_group()
+
+
+def measure_e2e(comms, n, nbytes, dt, ts, stream, dev):
+    """Host-resident end to end: pinned H2D of every rank's input, AllReduce, D2H."""
+    import torch
+    cnt = nbytes // ts
+    host_in = [torch.empty(nbytes // 4, dtype=torch.float32).uniform_(-1, 1).pin_memory() for _ in range(n)]
+    host_out = [torch.empty(nbytes // 4, dtype=torch.float32).pin_memory() for _ in range(n)]
+    dbufs = [torch.empty(nbytes // 4, dtype=torch.float32, device=dev) for _ in range(n)]
+    reps = 10
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for i in range(n):
+            dbufs[i].copy_(host_in[i], non_blocking=True)
+        with M.group():
+            for c, b in zip(comms, dbufs):
+                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+        for i in range(n):
+            host_out[i].copy_(dbufs[i], non_blocking=True)
+    torch.cuda.synchronize()
+    t = (time.perf_counter() - t0) / reps
+    algbw = nbytes / t / 1e9
+    return {"bytes": nbytes, "ms": round(t * 1e3, 4), "algbw": round(algbw, 3),
+            "busbw": round(algbw * 2 * (n - 1) / n, 3)}
+
+
+if __name__ == "__main__":
+    main()
