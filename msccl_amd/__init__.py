@@ -107,10 +107,12 @@ def version() -> int:
 def get_unique_id() -> bytes:
     uid = UniqueId()
     _check(lib().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
-    return bytes(uid.internal)
+    return ctypes.string_at(ctypes.addressof(uid), 128)  # .internal would stop at the first NUL
 
 
 def _uid(b: bytes) -> UniqueId:
+    if len(b) != 128:
+        raise ValueError("ncclUniqueId must be 128 bytes")
     u = UniqueId()
     ctypes.memmove(ctypes.addressof(u), b, 128)
     return u

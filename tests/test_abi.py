@@ -1,0 +1,58 @@
+"""The C-ABI library loads and exports every function include/*.h declares (no GPU calls)."""
+import ctypes
+import glob
+import os
+import re
+import subprocess
+
+import msccl_amd as M
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(h).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?\w+\*?\s+\*?(\w+)\s*\(", text, flags=re.M):
+            if m.group(1) not in ("if", "return", "sizeof"):
+                names.add(m.group(1))
+    return names
+
+
+def test_all_declared_symbols_exported():
+    names = declared_functions()
+    assert {"ncclAllReduce", "ncclReduceScatter", "ncclAllGather", "ncclCommInitRank", "ncclCommInitAll",
+            "ncclGroupStart", "ncclGroupEnd", "mscclAmdAlgoJson"} <= names
+    lib = M.lib()
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.check_output(["nm", "-D", "--defined-only", M.LIB_PATH]).decode()
+    exported = set(l.split()[-1] for l in out.splitlines() if " T " in l)
+    assert names <= exported
+
+
+def test_version_and_error_strings():
+    assert M.version() == 21212
+    lib = M.lib()
+    assert lib.ncclGetErrorString(0) == b"no error"
+    assert lib.ncclGetErrorString(5) == b"invalid usage"
+
+
+def test_invalid_arguments_without_gpu():
+    lib = M.lib()
+    # null comm pointer / invalid comm handle are argument errors, no device call happens
+    assert lib.ncclCommInitRank(None, 2, M.UniqueId(), 0) == 4
+    assert lib.ncclAllReduce(None, None, 0, 7, 0, None, None) == 4
+    assert lib.ncclCommDestroy(None) == 0
+    assert lib.ncclGroupEnd() == 5  # not in a group
+
+
+def test_enum_values_match_reference():
+    hdr = open(os.path.join(ROOT, "include", "nccl.h")).read()
+    for name, val in [("ncclSum", 0), ("ncclProd", 1), ("ncclMax", 2), ("ncclMin", 3), ("ncclAvg", 4),
+                      ("ncclInt8", 0), ("ncclUint8", 1), ("ncclInt32", 2), ("ncclUint32", 3), ("ncclInt64", 4),
+                      ("ncclUint64", 5), ("ncclFloat16", 6), ("ncclFloat32", 7), ("ncclFloat64", 8),
+                      ("ncclBfloat16", 9), ("ncclInvalidUsage", 5), ("ncclUnhandledCudaError", 1)]:
+        assert re.search(r"\b%s\s*=\s*%d\b" % (name, val), hdr), name

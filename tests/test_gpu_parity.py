@@ -1,0 +1,126 @@
+"""GPU parity: the HIP interpreter through the C-ABI vs the CPU oracle, bit-exact.
+
+Ranks are co-resident on cuda:0 (ncclCommInitAll with a repeated device) so one MI355X runs
+every rank of the schedule; the kernels, FIFOs, head/tail credits and dependency flags are the
+same as over xGMI.  Every comparison is bit-for-bit against oracle/sim.py on the same seeded
+inputs (the reference's association order is part of the contract).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from msccl_amd import xmlgen
+from oracle import loader as L
+from oracle import numerics as N
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
+
+
+def check(xml, n, coll, count, dt, op=0, inplace=True, seed=1, mode="uniform", iters=1):
+    from tests.gpu_harness import run_collective
+    gpu, ora, _ = run_collective(xml, n, coll, count, dt, op, inplace, seed, mode, iters)
+    for r in range(n):
+        g, o = gpu[r].view(np.uint8), np.asarray(ora[r]).view(np.uint8)
+        if not np.array_equal(g, o):
+            bad = np.nonzero(g != o)[0]
+            raise AssertionError("rank %d: %d differing bytes, first at byte %d" % (r, len(bad), bad[0]))
+
+
+# all-pairs AllReduce: protocol x dtype x size (small reduce path, multi-iteration, maxAllowedCount split)
+@pytest.mark.parametrize("proto", ["LL", "Simple"])
+@pytest.mark.parametrize("dt", [7, 6, 9])
+@pytest.mark.parametrize("n,inst,count", [
+    (2, 1, 4 * 8),            # 128 B fp32: smallest C2 point, per-element reduce path
+    (2, 4, 16 * 1000),        # small path (nelem*count < nthreads)
+    (2, 4, 1 << 18),          # multi-iteration, maxAllowedCount = 1
+    (2, 16, (1 << 20) + 16 * 64),
+    (4, 2, 32 * 4099),        # odd per-chunk size: unaligned 16-B packs, element tails
+    (8, 4, 256 * 300),
+])
+def test_allpairs_allreduce(proto, dt, n, inst, count):
+    check(xmlgen.allreduce_allpairs(n, inst, proto), n, L.ALLREDUCE, count, dt)
+
+
+@pytest.mark.parametrize("proto", ["LL", "Simple"])
+def test_allpairs_out_of_place(proto):
+    check(xmlgen.allreduce_allpairs(8, 2, proto, inplace=False), 8, L.ALLREDUCE, 128 * 513, 7, inplace=False)
+
+
+@pytest.mark.parametrize("proto,dt", [("Simple", 9), ("LL", 7), ("Simple", 6)])
+def test_ring_allreduce(proto, dt):
+    check(xmlgen.allreduce_ring(8, 4, proto), 8, L.ALLREDUCE, 32 * 20000, dt)
+
+
+def test_ring_c4_shape_large():
+    """C4 shape at reduced size: 8-rank ring, Simple, bf16, multi-chunk (2 interpreter iterations)."""
+    check(xmlgen.allreduce_ring(8, 8, "Simple"), 8, L.ALLREDUCE, 64 * (1 << 16) + 64 * 7, 9)
+
+
+@pytest.mark.parametrize("op", [1, 2, 3])
+@pytest.mark.parametrize("dt", [7, 6, 9, 8])
+def test_other_ops(op, dt):
+    check(xmlgen.allreduce_allpairs(4, 2, "LL"), 4, L.ALLREDUCE, 32 * 777, dt, op=op)
+
+
+@pytest.mark.parametrize("dt", [0, 1, 2, 3, 4, 5])
+def test_integer_types(dt):
+    check(xmlgen.allreduce_allpairs(4, 1, "Simple"), 4, L.ALLREDUCE, 16 * 1001, dt, mode="exact")
+    check(xmlgen.allreduce_allpairs(2, 2, "LL"), 2, L.ALLREDUCE, 8 * 999, dt, op=2)
+
+
+@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("Simple", True)])
+def test_reduce_scatter(proto, inplace):
+    check(xmlgen.reduce_scatter_allpairs(8, 2, proto, inplace=inplace), 8, L.REDUCE_SCATTER, 2 * 50000, 7,
+          inplace=inplace)
+
+
+@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("LL", False)])
+def test_all_gather(proto, inplace):
+    check(xmlgen.allgather_allpairs(8, 2, proto, inplace=inplace), 8, L.ALLGATHER, 2 * 33333, 7, inplace=inplace)
+
+
+def test_repeated_launches_persist_fifo_state():
+    """Many launches on the same communicators: step counters, LL flags and workIndex carry over."""
+    check(xmlgen.allreduce_allpairs(4, 2, "LL"), 4, L.ALLREDUCE, 32 * 64, 7, mode="exact", iters=40)
+    check(xmlgen.allreduce_allpairs(4, 2, "Simple"), 4, L.ALLREDUCE, 32 * 640, 7, mode="exact", iters=25)
+
+
+def test_rccl_allpairs_schedules(rccl_xmls):
+    for f in rccl_xmls:
+        base = os.path.basename(f)
+        if not base.startswith("allreduce-allpairs-8n"):
+            continue
+        text = open(f).read()
+        a = L.parse_xml(text, 0, 8)
+        count = a.nchunksperloop * (16 if a.proto == L.PROTO_LL else 600)
+        if a.proto == L.PROTO_LL:
+            count = min(count, (a.maxBytes - 1) // 2 // a.nchunksperloop * a.nchunksperloop)
+        check(text, 8, L.ALLREDUCE, count, 6, inplace=bool(a.inplace))
+
+
+def test_rccl_ring16_ll(rccl_xmls):
+    p = "/opt/rocm/share/rccl/msccl-unit-test-algorithms/all-reduce-ring-ll.xml"
+    if not os.path.exists(p):
+        pytest.skip("fixture missing")
+    text = open(p).read()
+    check(text, 16, L.ALLREDUCE, 384 * 4, 7)
+
+
+@pytest.mark.parametrize("name", ["ap2_ll_f32", "ap4_ll_bf16", "ring8_simple_bf16", "rs8_simple_f32",
+                                  "ag8_ll_f32", "ap8_ll_f16_rccl32tb", "ap2_ll_i32_exact"])
+def test_golden_vectors_on_gpu(name):
+    from tests.golden import make_golden as G
+    from tests.gpu_harness import run_collective
+    case = [c for c in G.CASES if c[0] == name][0]
+    _, xf, n, coll, count, dt, op, inplace, mode = case
+    try:
+        xml = xf()
+    except OSError:
+        pytest.skip("source XML missing")
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", name + ".npz"))
+    gpu, _, ins = run_collective(xml, n, coll, count, dt, op, inplace, seed=7, mode=mode)
+    assert np.array_equal(np.stack(ins), z["inputs"])
+    for r in range(n):
+        assert np.array_equal(gpu[r].view(np.uint8), z["outputs"][r].view(np.uint8)), r

@@ -1,0 +1,167 @@
+"""GPU runtime behaviour: multi-process ranks over hipIpc, API edge cases, failure handling."""
+import os
+
+import numpy as np
+import pytest
+
+import msccl_amd as M
+from msccl_amd import xmlgen
+from oracle import loader as L
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
+
+
+def _rank_proc(rank, world, xml_path, count, q_in, q_out):
+    import torch
+    os.environ["MSCCL_XML_FILES"] = xml_path
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "30"
+    torch.cuda.set_device(0)
+    if rank == 0:
+        uid = M.get_unique_id()
+        for _ in range(world - 1):
+            q_in.put(uid)
+    else:
+        uid = None
+    if uid is None:
+        uid = q_in.get(timeout=60)
+    from tests.gpu_harness import gen_inputs, to_torch
+    x = gen_inputs(world, count, 7, 5)[rank]
+    comm = M.Comm.init_rank(world, uid, rank)
+    t = to_torch(x, torch.device("cuda:0"))
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        comm.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, s)
+    torch.cuda.synchronize()
+    err = comm.async_error()
+    out = t.cpu().numpy()
+    comm.destroy()
+    q_out.put((rank, err, out))
+
+
+@pytest.mark.parametrize("proto", ["LL", "Simple"])
+def test_multiprocess_ipc_ranks(tmp_path, proto):
+    """Two processes, one rank each, FIFOs mapped with hipIpcOpenMemHandle (the multi-GPU path)."""
+    import torch.multiprocessing as mp
+    from tests.gpu_harness import gen_inputs
+    from oracle import plan as P, sim as S
+    world, count = 2, 16 * 4096
+    xml = xmlgen.allreduce_allpairs(world, 4, proto)
+    p = tmp_path / "ap.xml"
+    p.write_text(xml)
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_rank_proc, args=(r, world, str(p), count, q_in, q_out)) for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, out = q_out.get(timeout=300)
+        res[r] = (err, out)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    algos = [L.parse_xml(xml, r, world) for r in range(world)]
+    call = P.Call(L.ALLREDUCE, count, 7, 0, world, 0, True)
+    plan = P.make_plan([algos[0]], call, 0)
+    ins = gen_inputs(world, count, 7, 5)
+    for _ in range(3):
+        ins, _st = S.run(algos, plan, ins, [None] * world, L.ALLREDUCE, True)
+    for r in range(world):
+        assert res[r][0] == 0
+        assert np.array_equal(res[r][1].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
+
+
+def test_single_rank_is_a_copy():
+    import torch
+    comm = M.Comm.init_all([0])[0]
+    try:
+        a = torch.randn(1 << 18, device="cuda")
+        b = torch.zeros_like(a)
+        s = torch.cuda.current_stream().cuda_stream
+        comm.all_reduce(a.data_ptr(), b.data_ptr(), a.numel(), M.FLOAT32, M.SUM, s)   # C1: D2D copy
+        comm.all_reduce(a.data_ptr(), a.data_ptr(), a.numel(), M.FLOAT32, M.SUM, s)   # in place: no-op
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        assert comm.nranks == 1 and comm.rank == 0 and comm.device == 0
+    finally:
+        comm.destroy()
+
+
+def test_no_matching_algorithm_and_zero_count(tmp_path):
+    import torch
+    p = tmp_path / "ap.xml"
+    p.write_text(xmlgen.allreduce_allpairs(2, 4, "LL", max_bytes=1 << 20))
+    os.environ["MSCCL_XML_FILES"] = str(p)
+    comms = M.Comm.init_all([0, 0])
+    try:
+        a = [torch.zeros(1 << 20, device="cuda") for _ in comms]
+        s = torch.cuda.current_stream().cuda_stream
+        with pytest.raises(M.NcclError) as ei:
+            with M.group():
+                for c, t in zip(comms, a):
+                    c.all_reduce(t.data_ptr(), t.data_ptr(), 24, M.FLOAT32, M.SUM, s)  # 24 % 16 != 0
+        assert ei.value.code == 5
+        with pytest.raises(M.NcclError):
+            comms[0].all_reduce(a[0].data_ptr(), a[0].data_ptr(), 1 << 19, M.FLOAT32, M.SUM, s)  # >= maxBytes
+        with M.group():
+            for c, t in zip(comms, a):
+                c.all_reduce(t.data_ptr(), t.data_ptr(), 0, M.FLOAT32, M.SUM, s)
+        torch.cuda.synchronize()
+        info = comms[0].info()
+        assert info["nranks"] == 2 and info["sendConns"] == 4 and info["recvConns"] == 4
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_timeout_reports_async_error(tmp_path):
+    """A rank whose peer never launches times out in-kernel and reports through ncclCommGetAsyncError."""
+    import torch
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "2"
+    p = tmp_path / "ap.xml"
+    p.write_text(xmlgen.allreduce_allpairs(2, 1, "LL"))
+    os.environ["MSCCL_XML_FILES"] = str(p)
+    comms = M.Comm.init_all([0, 0])
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "20"
+    try:
+        t = torch.ones(1024, device="cuda")
+        s = torch.cuda.current_stream().cuda_stream
+        comms[0].all_reduce(t.data_ptr(), t.data_ptr(), 1024, M.FLOAT32, M.SUM, s)  # rank 1 never joins
+        torch.cuda.synchronize()
+        assert comms[0].async_error() == 2  # ncclSystemError
+    finally:
+        comms[0].abort()
+        comms[1].destroy()
+
+
+def test_stream_ordering_separate_streams():
+    """Co-resident ranks issuing on different streams are fused and ordered with events."""
+    import torch
+    from tests.gpu_harness import gen_inputs, to_torch
+    from oracle import plan as P, sim as S
+    xml = xmlgen.allreduce_allpairs(2, 2, "Simple")
+    path = "/tmp/msccl_streams_%d.xml" % os.getpid()
+    open(path, "w").write(xml)
+    os.environ["MSCCL_XML_FILES"] = path
+    comms = M.Comm.init_all([0, 0])
+    try:
+        count = 8 * 5000
+        ins = gen_inputs(2, count, 7, 9)
+        dev = torch.device("cuda:0")
+        ts = [to_torch(x, dev) for x in ins]
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        torch.cuda.synchronize()
+        with M.group():
+            for c, t, st in zip(comms, ts, streams):
+                c.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, st.cuda_stream)
+        for st in streams:
+            st.synchronize()
+        algos = [L.parse_xml(xml, r, 2) for r in range(2)]
+        plan = P.make_plan([algos[0]], P.Call(L.ALLREDUCE, count, 7, 0, 2, 0, True), 0)
+        want, _ = S.run(algos, plan, [x.copy() for x in ins], [None, None], L.ALLREDUCE, True)
+        for r in range(2):
+            assert np.array_equal(ts[r].cpu().numpy().view(np.uint32), want[r].view(np.uint32))
+    finally:
+        for c in comms:
+            c.destroy()
