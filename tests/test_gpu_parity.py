@@ -94,9 +94,11 @@ def test_rccl_allpairs_schedules(rccl_xmls):
             continue
         text = open(f).read()
         a = L.parse_xml(text, 0, 8)
-        count = a.nchunksperloop * (16 if a.proto == L.PROTO_LL else 600)
-        if a.proto == L.PROTO_LL:
-            count = min(count, (a.maxBytes - 1) // 2 // a.nchunksperloop * a.nchunksperloop)
+        ncpl = a.nchunksperloop
+        lo = -(-a.minBytes // 2 // ncpl) * ncpl          # fp16 elements, multiple of ncpl, >= minBytes
+        count = max(ncpl * 16, lo)
+        count = min(count, (a.maxBytes - 1) // 2 // ncpl * ncpl)
+        assert a.minBytes <= 2 * count < a.maxBytes
         check(text, 8, L.ALLREDUCE, count, 6, inplace=bool(a.inplace))
 
 
