@@ -29,8 +29,10 @@ struct ConnKey {
 // Per-rank transport table exchanged during init: for every (channel, peer) the offsets,
 // inside this rank's transport arena, of the receive FIFOs / tail word (this rank receiving
 // from peer) and of the head word (this rank sending to peer).  -1 = no connection.
+// Sub-connection k (0 <= k < maxSplit) of a key sits at base + k * stride.
 struct PeerOffsets {
   int64_t recvLL, recvSimple, recvTail, sendHead;
+  int64_t llStride, simpleStride, wordStride, pad;
 };
 
 struct DevAlgoHost {
@@ -49,6 +51,9 @@ struct ncclComm {
   std::vector<msccl::Algorithm> algos;
   std::vector<msccl::Registration> regs;
   std::vector<msccl::DevAlgoHost> devAlgos;
+  std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
+  int maxSplit = 1;                // sub-connections per (channel, peer)
+  int coResident = 1;              // ranks of this communicator on this rank's GPU
 
   // transport
   std::vector<msccl::ConnKey> sendKeys, recvKeys;

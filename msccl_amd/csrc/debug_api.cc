@@ -74,7 +74,10 @@ int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
   o << "],\"sendConns\":" << comm->sendKeys.size() << ",\"recvConns\":" << comm->recvKeys.size()
     << ",\"arenaBytes\":" << comm->arenaSize << ",\"scratchBytes\":" << comm->scratchSize
     << ",\"llSlotLines\":" << comm->llSlotLines << ",\"simpleSlotBytes\":" << comm->simpleSlotBytes
-    << ",\"workIndex\":" << comm->workIndex << "}";
+    << ",\"workIndex\":" << comm->workIndex << ",\"maxSplit\":" << comm->maxSplit
+    << ",\"coResident\":" << comm->coResident << ",\"algoSplit\":[";
+  for (size_t i = 0; i < comm->algoSplit.size(); i++) o << (i ? "," : "") << comm->algoSplit[i];
+  o << "]}";
   return putOut(o.str(), out, outLen);
 }
 

@@ -8,7 +8,11 @@
 //     the sender's memory and a tail word in the receiver's memory; the sender writes the
 //     FIFO over xGMI (peer pointer or hipIpc mapping);
 //   * a launch may carry the work of several co-resident ranks (ranks that share one GPU):
-//     RankWork[i] owns blocks [blockBase, blockBase + nBlocks).
+//     RankWork[i] owns blocks [blockBase, blockBase + nBlocks);
+//   * one XML thread block may run as `split` workgroups: workgroup k of a tb owns the k-th
+//     1/split of the 16-B packs of every primitive call and its own sub-connection (FIFO,
+//     head/tail words, step counter) and dependency flag, so the values produced are the
+//     same as with one workgroup (the split is by element, every element keeps its order).
 #pragma once
 #include <stdint.h>
 
@@ -17,7 +21,8 @@ namespace msccl {
 constexpr int kFifoSteps = 8;          // NCCL_STEPS
 constexpr int kMaxLaunchRanks = 16;    // ranks fused into one launch (same device, same group)
 constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag padding)
-constexpr int kFlagSlots = 256;        // >= MSCCL_MAX_NUM_THREAD_BLOCKS
+constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
+constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kMaxSplit
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
 
 // LL FIFO line (ncclLLFifoLine, devcomm.h:35-48): two 8-B {4-B data, 4-B flag} granules.
@@ -68,6 +73,8 @@ struct DevComm {
   volatile uint32_t* abortFlag; // host-mapped
   uint32_t* errWord;            // host-mapped: 0 ok, else error code (1 timeout, 2 bad program)
   uint64_t timeoutTicks;        // s_memrealtime ticks (100 MHz)
+  int32_t maxSplit;             // sub-connections per (channel, peer): conn k of key c = send[c*maxSplit+k]
+  int32_t pad;
 };
 
 // One rank's share of a launch (the reference passes ncclDevComm* + a 64-B ncclWorkElem,
@@ -84,10 +91,10 @@ struct RankWork {
   int64_t minChunk;             // LL: nthreads*8/sizeof(T); Simple: rounding unit (nthreads-32)*8/sizeof(T)
   uint32_t workIndex;
   int16_t blockBase;
-  int16_t nBlocks;
+  int16_t nBlocks;              // workgroups = XML thread blocks x split
   int16_t refNthreads;          // reference nthreads (small-reduce switch, chunk rounding)
   uint8_t maxAllowedCount;
-  uint8_t pad;
+  uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
 };
 
 struct LaunchArgs {

@@ -1,17 +1,27 @@
-// MSCCL schedule interpreter for gfx950 (one workgroup = one XML thread block).
+// MSCCL schedule interpreter for gfx950.
 //
 // Behaviour follows the reference interpreter collectives/device/msccl_interpreter.h:66-205:
 //   * outer loop over gridOffset in steps of chunkSize; per-protocol realChunkSize/nelem
 //     (msccl_interpreter.h:105-113);
 //   * per transfer: wait on dependency flags COMPUTE_FLAG(workIndex, iter, step) of other
-//     workgroups of the same rank (123-140), split `count` by mscclMaxAllowedCount (146-150),
+//     thread blocks of the same rank (123-140), split `count` by mscclMaxAllowedCount (146-150),
 //     dispatch to the primitive, publish the own flag when hasdep (198-201);
 //   * reductions: LL order d(+)s0(+)s1.. (prims_ll.h:347-362), Simple order (s0(+)s1..)(+)d
 //     (prims_simple.h:258-263), per-element d-first path when thisNelem < nthreads (157-170);
 //   * recv-reduce: LL fn(peer, local) (prims_ll.h:282-287), Simple fn(local, peer).
-// Implementation is MI355X-native: wave64 workgroups of kNT threads, 16-B packs per lane,
-// buffer loads/stores with explicit cache-policy bits, LL lines polled two at a time with a
-// single wait, FIFO flow control with head/tail words in uncached memory, bounded spins.
+//
+// MI355X-native execution: wave64 workgroups of kNT threads, 16-B packs per lane, buffer
+// loads/stores with explicit cache-policy bits, LL lines polled two at a time with a single
+// wait, FIFO flow control through head/tail words in uncached memory, bounded spins.
+//
+// Work split.  One XML thread block may run as `split` workgroups.  Workgroup k owns, inside
+// every MSCCL chunk, the k-th contiguous 1/split of that chunk's 16-B packs ("position within
+// the chunk").  Every data movement of an MSCCL schedule preserves an element's position
+// inside its chunk (a transfer moves whole chunks, offsets are chunk-granular), so workgroup k
+// only ever reads what workgroup k of the same or another thread block (or rank) wrote: each
+// workgroup has its own sub-connection (FIFO, head/tail, step counter) and its own dependency
+// flag, and no transfer ever needs another workgroup's data.  A launch uses split = 1 whenever
+// a chunk is not a whole number of packs.
 #pragma once
 #include "primitives.h"
 
@@ -38,6 +48,20 @@ __device__ __forceinline__ uint64_t computeFlag(uint64_t workIndex, uint64_t ite
 // consecutive lines and its second lines in the next 64, so a wave's stores/loads of one half
 // are a contiguous 1 KiB.
 __device__ __forceinline__ int llLineIdx(int p, int h) { return ((p >> 6) << 7) + (h << 6) + (p & 63); }
+
+// The packs of one primitive call that this workgroup owns: `count` chunks of Q packs each,
+// positions [q0, q0 + Lq) of every chunk.  Sub-local pack s maps to op pack bufPack(s).
+struct Shape {
+  int n;      // elements of the whole call (bound for tails)
+  int Q;      // packs per chunk
+  int q0, Lq; // owned positions
+  int npk;    // owned packs = count * Lq
+  __device__ __forceinline__ int bufPack(int s) const {
+    if (Lq == Q) return s;  // split == 1 or a whole chunk: contiguous
+    int c = s / Lq;
+    return c * Q + q0 + (s - c * Lq);
+  }
+};
 
 template <typename T, int OP, int PROTO>
 struct Interp {
@@ -99,15 +123,16 @@ struct Interp {
     for (int i = 0; i < PE; i++)
       if (i < ne) stElem<T>(r, (uint32_t)(e0 + i) * TS, v[i]);
   }
-  __device__ __forceinline__ u32x4 loadPack(__amdgpu_buffer_rsrc_t r, bool vec, int p, int nelem) {
-    int e0 = p * PE;
-    int ne = nelem - e0;
+  // op pack B of a buffer holding n elements
+  __device__ __forceinline__ u32x4 loadPack(__amdgpu_buffer_rsrc_t r, bool vec, int B, int n) {
+    int e0 = B * PE;
+    int ne = n - e0;
     if (vec && ne >= PE) return ld16<kAuxLocal>(r, (uint32_t)e0 * TS);
     return loadPartial(r, e0, ne < PE ? ne : PE);
   }
-  __device__ __forceinline__ void storePack(__amdgpu_buffer_rsrc_t r, bool vec, int p, int nelem, u32x4 x) {
-    int e0 = p * PE;
-    int ne = nelem - e0;
+  __device__ __forceinline__ void storePack(__amdgpu_buffer_rsrc_t r, bool vec, int B, int n, u32x4 x) {
+    int e0 = B * PE;
+    int ne = n - e0;
     if (vec && ne >= PE) st16<kAuxLocal>(r, (uint32_t)e0 * TS, x);
     else storePartial(r, e0, ne < PE ? ne : PE, x);
   }
@@ -115,10 +140,9 @@ struct Interp {
 
   // ---------------------------------------------------------------- LL protocol
   template <int RECV, int SEND, int SRC, int DST>
-  __device__ void llOp(const T* src, T* dst, int nelem) {
+  __device__ void llOp(const T* src, T* dst, const Shape& s) {
     constexpr int E = 8 / TS;  // elements per line
-    const int nlines = (nelem + E - 1) / E;
-    const int npacks = (nlines + 1) / 2;
+    const int nlinesFull = (s.n + E - 1) / E;
     if (SEND) waitSendCredit();
     LLLine* rslot = nullptr;
     __amdgpu_buffer_rsrc_t srs, drs, frs;
@@ -134,11 +158,12 @@ struct Interp {
     if (SRC) srs = makeRsrc(src);
     if (DST) drs = makeRsrc(dst);
     const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
-    for (int p = tid; p < npacks; p += kNT) {
+    for (int p = tid; p < s.npk; p += kNT) {
+      const int B = s.bufPack(p);
       const int l0 = llLineIdx(p, 0), l1 = llLineIdx(p, 1);
-      const bool two = 2 * p + 1 < nlines;
+      const bool two = 2 * B + 1 < nlinesFull;
       u32x4 data = {0, 0, 0, 0}, v;
-      if (SRC) data = loadPack(srs, vec, p, nelem);
+      if (SRC) data = loadPack(srs, vec, B, s.n);
       if (RECV) {
         u32x4 a, b = {0, 0, 0, 0};
         uint32_t spins = 0;
@@ -160,14 +185,15 @@ struct Interp {
         st16<kAuxFifo>(frs, (uint32_t)l0 * 16, (u32x4){v.x, sflag, v.y, sflag});
         if (two) st16<kAuxFifo>(frs, (uint32_t)l1 * 16, (u32x4){v.z, sflag, v.w, sflag});
       }
-      if (DST) storePack(drs, vec, p, nelem, v);
+      if (DST) storePack(drs, vec, B, s.n, v);
     }
     if (SEND) {
       if ((sendStep & kLLCleanMask) == kLLCleanMask) {
         // LL cleanup (prims_ll.h:90-97): stamp every unused line of the slot with this flag
         for (int l = tid; l < sc->llSlotLines; l += kNT) {
           int p = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
-          if (2 * p + h >= nlines) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
+          bool used = p < s.npk && 2 * s.bufPack(p) + h < nlinesFull;
+          if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
         }
       }
       sendStep++;
@@ -181,11 +207,15 @@ struct Interp {
 
   // ---------------------------------------------------------------- Simple protocol
   template <int RECV, int SEND, int SRC, int DST>
-  __device__ void simpleOp(const T* src, T* dst, int nelem) {
+  __device__ void simpleOp(const T* src, T* dst, const Shape& s) {
     const int slotBytes = SEND ? sc->simpleSlotBytes : rc->simpleSlotBytes;
-    const int sliceElems = slotBytes / TS;
-    for (int off = 0; off < nelem; off += sliceElems) {
-      const int n = nelem - off < sliceElems ? nelem - off : sliceElems;
+    const int slicePacks = slotBytes / 16;
+    __amdgpu_buffer_rsrc_t srs, drs, rrs, frs;
+    if (SRC) srs = makeRsrc(src);
+    if (DST) drs = makeRsrc(dst);
+    const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
+    for (int s0 = 0; s0 < s.npk; s0 += slicePacks) {
+      const int s1 = s.npk - s0 < slicePacks ? s.npk : s0 + slicePacks;
       if (tid == 0) {
         uint32_t spins = 0;
         if (RECV)
@@ -197,24 +227,20 @@ struct Interp {
       }
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      __amdgpu_buffer_rsrc_t srs, drs, rrs, frs;
-      if (SRC) srs = makeRsrc(src + off);
-      if (DST) drs = makeRsrc(dst + off);
       if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
       if (SEND) frs = makeRsrc(sc->simple + (sendStep % kFifoSteps) * (uint64_t)slotBytes);
-      const bool vec = (!SRC || aligned16(src + off)) && (!DST || aligned16(dst + off));
-      const int npacks = (n + PE - 1) / PE;
-      for (int p = tid; p < npacks; p += kNT) {
+      for (int p = s0 + tid; p < s1; p += kNT) {
+        const int B = s.bufPack(p);
         u32x4 data = {0, 0, 0, 0}, v;
-        if (SRC) data = loadPack(srs, vec, p, n);
+        if (SRC) data = loadPack(srs, vec, B, s.n);
         if (RECV) {
-          u32x4 peer = ld16<kAuxFifo>(rrs, (uint32_t)p * 16);
+          u32x4 peer = ld16<kAuxFifo>(rrs, (uint32_t)(p - s0) * 16);
           v = SRC ? F::pack(data, peer) : peer;
         } else {
           v = data;
         }
-        if (SEND) st16<kAuxFifo>(frs, (uint32_t)p * 16, v);
-        if (DST) storePack(drs, vec, p, n, v);
+        if (SEND) st16<kAuxFifo>(frs, (uint32_t)(p - s0) * 16, v);
+        if (DST) storePack(drs, vec, B, s.n, v);
       }
       drainStores();
       __syncthreads();
@@ -228,25 +254,30 @@ struct Interp {
   }
 
   template <int RECV, int SEND, int SRC, int DST>
-  __device__ __forceinline__ void op(const T* src, T* dst, int nelem) {
-    if constexpr (PROTO == pSimple) simpleOp<RECV, SEND, SRC, DST>(src, dst, nelem);
-    else llOp<RECV, SEND, SRC, DST>(src, dst, nelem);
+  __device__ __forceinline__ void op(const T* src, T* dst, const Shape& s) {
+    if constexpr (PROTO == pSimple) simpleOp<RECV, SEND, SRC, DST>(src, dst, s);
+    else llOp<RECV, SEND, SRC, DST>(src, dst, s);
   }
 
   // ---------------------------------------------------------------- local ops
-  __device__ void localCopy(const T* src, T* dst, int nelem) {
+  __device__ void localCopy(const T* src, T* dst, const Shape& s) {
     __amdgpu_buffer_rsrc_t srs = makeRsrc(src), drs = makeRsrc(dst);
     const bool vec = aligned16(src) && aligned16(dst);
-    const int npacks = (nelem + PE - 1) / PE;
-    for (int p = tid; p < npacks; p += kNT) storePack(drs, vec, p, nelem, loadPack(srs, vec, p, nelem));
+    for (int p = tid; p < s.npk; p += kNT) {
+      const int B = s.bufPack(p);
+      storePack(drs, vec, B, s.n, loadPack(srs, vec, B, s.n));
+    }
   }
 
-  // srcOffs[r] are element offsets from srcBase; MSCCL_MAX_REDUCE_FUSION = 16
-  __device__ void reduce(const T* srcBase, const int64_t* srcOffs, int nsrc, T* dst, int nelem) {
-    if (nelem < refNthreads) {
+  // srcOffs[r]: element offsets of the reduction sources from srcBase (MSCCL_MAX_REDUCE_FUSION
+  // = 16).  The per-element path is chosen on the whole call's element count, as in the reference.
+  __device__ void reduce(const T* srcBase, const int64_t* srcOffs, int nsrc, T* dst, const Shape& s) {
+    if (s.n < refNthreads) {
       // per-element path, d first: o = fn(s_r, o) (msccl_interpreter.h:157-170)
       __amdgpu_buffer_rsrc_t drs = makeRsrc(dst), srs = makeRsrc(srcBase);
-      for (int e = tid; e < nelem; e += kNT) {
+      for (int k = tid; k < s.npk * PE; k += kNT) {
+        const int e = s.bufPack(k / PE) * PE + (k % PE);
+        if (e >= s.n) continue;
         T o = ldElem<T>(drs, (uint32_t)e * TS);
 #pragma unroll
         for (int r = 0; r < 16; r++)
@@ -260,16 +291,16 @@ struct Interp {
 #pragma unroll
     for (int r = 0; r < 16; r++)
       if (r < nsrc) vec = vec && aligned16(srcBase + srcOffs[r]);
-    const int npacks = (nelem + PE - 1) / PE;
-    for (int p = tid; p < npacks; p += kNT) {
-      u32x4 d = loadPack(drs, vec, p, nelem);
+    for (int p = tid; p < s.npk; p += kNT) {
+      const int B = s.bufPack(p);
+      u32x4 d = loadPack(drs, vec, B, s.n);
       u32x4 acc;
       if constexpr (PROTO == pSimple) {
 #pragma unroll
         for (int r = 0; r < 16; r++) {
           if (r < nsrc) {
-            u32x4 s = loadPack(makeRsrc(srcBase + srcOffs[r]), vec, p, nelem);
-            acc = r == 0 ? s : F::pack(acc, s);
+            u32x4 x = loadPack(makeRsrc(srcBase + srcOffs[r]), vec, B, s.n);
+            acc = r == 0 ? x : F::pack(acc, x);
           }
         }
         acc = F::pack(acc, d);
@@ -277,19 +308,21 @@ struct Interp {
         acc = d;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-          if (r < nsrc) acc = F::pack(acc, loadPack(makeRsrc(srcBase + srcOffs[r]), vec, p, nelem));
+          if (r < nsrc) acc = F::pack(acc, loadPack(makeRsrc(srcBase + srcOffs[r]), vec, B, s.n));
         }
       }
-      storePack(drs, vec, p, nelem, acc);
+      storePack(drs, vec, B, s.n, acc);
     }
   }
 
   // ---------------------------------------------------------------- the interpreter loop
-  __device__ void run(const RankWork& w, int bid) {
+  __device__ void run(const RankWork& w, int bid, int sub) {
     tid = threadIdx.x;
     comm = w.comm;
     refNthreads = w.refNthreads;
     t0 = __builtin_amdgcn_s_memrealtime();
+    const int split = w.split;
+    const int maxSplit = comm->maxSplit;
     const DevTbHeader hd = w.tbs[bid];
     // stage the tb program in LDS
     const DevTransfer* gtr = (const DevTransfer*)(w.blob + hd.blobOffset);
@@ -300,8 +333,8 @@ struct Interp {
       sh->depStep[i] = gdep[hd.ndeps + i];
     }
     for (int i = tid; i < hd.nreds; i += kNT) sh->red[i] = gdep[2 * hd.ndeps + i];
-    sc = hd.sendConn >= 0 ? comm->send + hd.sendConn : nullptr;
-    rc = hd.recvConn >= 0 ? comm->recv + hd.recvConn : nullptr;
+    sc = hd.sendConn >= 0 ? comm->send + (size_t)hd.sendConn * maxSplit + sub : nullptr;
+    rc = hd.recvConn >= 0 ? comm->recv + (size_t)hd.recvConn * maxSplit + sub : nullptr;
     if (tid == 0) {
       sh->step[0] = sc ? sc->step : 0;
       sh->step[1] = rc ? rc->step : 0;
@@ -332,16 +365,21 @@ struct Interp {
       }
       real = (int)real;
       const int nelem = (int)(real < sizePer - grid ? real : sizePer - grid);
+      // this workgroup's positions inside every chunk of this iteration (nelem % PE == 0
+      // whenever split > 1: the host sets split = 1 otherwise)
+      const int Qc = (nelem + PE - 1) / PE;
+      const int q0 = (int)((int64_t)Qc * sub / split), q1 = (int)((int64_t)Qc * (sub + 1) / split);
       int step = 0;
       for (int i = 0; i < hd.nsteps; i++) {
         const DevTransfer t = sh->tr[i];
         if (t.numDeps > 0) {
+          // the same positions of the thread blocks this transfer depends on (interpreter.h:123-140)
           if (tid < t.numDeps) {
             const int db = sh->depBid[t.depPtr + tid];
             const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)sh->depStep[t.depPtr + tid]);
             uint32_t spins = 0;
             while (true) {
-              uint64_t cur = atomicLoadAgent(flags + (size_t)db * kFlagStride);
+              uint64_t cur = atomicLoadAgent(flags + ((size_t)db * split + sub) * kFlagStride);
               if (cur >= goal && (cur >> 24) == workIndex) break;
               if (spinAbort(spins)) break;
             }
@@ -355,21 +393,33 @@ struct Interp {
           const int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
           const int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;
           const int thisCount = mac < t.count - c ? mac : t.count - c;
-          const int n = nelem * thisCount;
+          Shape s;
+          s.n = nelem * thisCount;
+          if (split == 1) {
+            s.Q = (s.n + PE - 1) / PE;
+            s.q0 = 0;
+            s.Lq = s.Q;
+            s.npk = s.Q;
+          } else {
+            s.Q = Qc;
+            s.q0 = q0;
+            s.Lq = q1 - q0;
+            s.npk = thisCount * s.Lq;
+          }
           switch (t.type) {
-            case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, n); __syncthreads(); break;
-            case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, n); break;
-            case tRCS: op<1, 1, 0, 1>(nullptr, dstP + dstoff, n); break;
-            case tRRS: op<1, 1, 1, 0>(srcP + srcoff, nullptr, n); break;
-            case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, n); break;
-            case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, n); break;
-            case tCpy: localCopy(srcP + srcoff, dstP + dstoff, n); __syncthreads(); break;
+            case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
+            case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, s); break;
+            case tRCS: op<1, 1, 0, 1>(nullptr, dstP + dstoff, s); break;
+            case tRRS: op<1, 1, 1, 0>(srcP + srcoff, nullptr, s); break;
+            case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
+            case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
+            case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
             case tRe: {
               int64_t offs[16];
 #pragma unroll
               for (int r = 0; r < 16; r++)
                 offs[r] = r < t.numReds ? grid + (int64_t)(sh->red[t.redPtr + r] + c) * sizePer : 0;
-              reduce(srcP, offs, t.numReds, dstP + dstoff, n);
+              reduce(srcP, offs, t.numReds, dstP + dstoff, s);
               if (c == 0) step += t.numReds - 1;
               __syncthreads();
               break;
@@ -382,7 +432,8 @@ struct Interp {
         if (t.hasDep) {
           drainStores();
           __syncthreads();
-          if (tid == 0) atomicStoreAgent(flags + (size_t)bid * kFlagStride, computeFlag(workIndex, iter, step));
+          if (tid == 0)
+            atomicStoreAgent(flags + ((size_t)bid * split + sub) * kFlagStride, computeFlag(workIndex, iter, step));
         }
         step++;
       }
@@ -402,9 +453,10 @@ __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
   int r = 0;
   while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
   const RankWork& w = args.w[r];
+  const int local = b - w.blockBase;
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
-  it.run(w, b - w.blockBase);
+  it.run(w, local / w.split, local % w.split);
 }
 
 }  // namespace msccl

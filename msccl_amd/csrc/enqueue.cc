@@ -104,7 +104,12 @@ RankWork makeWork(Planned& p) {
   w.sizePerChunk = p.plan.sizePerChunk;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;
-  w.nBlocks = (int16_t)da.nBlocks;
+  // Workgroups of a split thread block own 16-B pack positions inside each chunk, so a split
+  // needs whole packs per chunk; sizePerChunk is identical on every rank, so all ranks agree.
+  int split = comm->algoSplit.empty() ? 1 : comm->algoSplit[p.plan.algoIndex];
+  if (p.plan.sizePerChunk % (16 / refTypeSize(p.plan.dtype)) != 0) split = 1;
+  w.split = (uint8_t)split;
+  w.nBlocks = (int16_t)(da.nBlocks * split);
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.workIndex = comm->workIndex++;

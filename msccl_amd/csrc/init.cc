@@ -7,10 +7,15 @@
 #include <mutex>
 #include <thread>
 
+#include <stdio.h>
+
+#include <algorithm>
+
 #include "bootstrap.h"
 #include "comm.h"
 #include "debug.h"
 #include "group.h"
+#include "plan.h"
 
 using namespace msccl;
 
@@ -68,8 +73,49 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
     NCCLCHECK(hipErr(hipMemset(comm->scratch, 0, scratch), "hipMemset scratch"));
     comm->scratchSize = scratch;
   }
-  if (comm->nRanks > 1) NCCLCHECK(transportPlan(comm));
   return ncclSuccess;
+}
+
+// What every rank contributes to the split decision (all ranks must reach the same splits).
+struct SplitRecord {
+  char host[64];
+  char bus[32];
+  int32_t nAlgos;
+  int32_t nBlocks[kMaxAlgos];
+};
+
+SplitRecord makeSplitRecord(ncclComm* comm) {
+  SplitRecord s;
+  memset(&s, 0, sizeof(s));
+  gethostname(s.host, sizeof(s.host) - 1);
+  if (hipDeviceGetPCIBusId(s.bus, sizeof(s.bus) - 1, comm->cudaDev) != hipSuccess)
+    snprintf(s.bus, sizeof(s.bus), "dev%d", comm->cudaDev);
+  s.nAlgos = (int32_t)comm->algos.size();
+  for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) s.nBlocks[a] = comm->algos[a].nBlocks;
+  return s;
+}
+
+void applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
+  int maxCo = 1;
+  for (auto& r : recs) {
+    int c = 0;
+    for (auto& q : recs) c += !strcmp(r.host, q.host) && !strcmp(r.bus, q.bus);
+    maxCo = std::max(maxCo, c);
+  }
+  const SplitRecord& mine = recs[comm->rank];
+  comm->coResident = 0;
+  for (auto& q : recs) comm->coResident += !strcmp(mine.host, q.host) && !strcmp(mine.bus, q.bus);
+  comm->algoSplit.assign(comm->algos.size(), 1);
+  comm->maxSplit = 1;
+  for (size_t a = 0; a < comm->algos.size(); a++) {
+    int mb = 0;
+    for (auto& r : recs)
+      if ((int)a < r.nAlgos) mb = std::max(mb, (int)r.nBlocks[a]);
+    comm->algoSplit[a] = chooseSplit(mb, maxCo);
+    comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
+  }
+  INFO(kSubInit, "rank %d: %d co-resident ranks per GPU (max), %d sub-connections per connection", comm->rank,
+       maxCo, comm->maxSplit);
 }
 
 ncclResult_t commFinish(ncclComm* comm) {
@@ -82,6 +128,7 @@ ncclResult_t commFinish(ncclComm* comm) {
   dc.abortFlag = comm->devAbort;
   dc.errWord = comm->devErr;
   dc.timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
+  dc.maxSplit = comm->maxSplit;
   NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
   NCCLCHECK(hipErr(hipMemcpy(comm->dComm, &dc, sizeof(dc), hipMemcpyHostToDevice), "hipMemcpy"));
   NCCLCHECK(hipErr(hipDeviceSynchronize(), "hipDeviceSynchronize"));
@@ -105,6 +152,13 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
   NCCLCHECK(commLocalSetup(comm));
   const int n = comm->nRanks;
   if (n > 1) {
+    SplitRecord srec = makeSplitRecord(comm);
+    std::vector<char> sall;
+    NCCLCHECK(sb->allgather(&srec, sizeof(srec), &sall));
+    std::vector<SplitRecord> recs(n);
+    memcpy(recs.data(), sall.data(), sizeof(SplitRecord) * n);
+    applySplits(comm, recs);
+    NCCLCHECK(transportPlan(comm));
     RankRecord rec;
     memset(&rec, 0, sizeof(rec));
     rec.pid = getpid();
@@ -242,6 +296,15 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
     c->cudaDev = dev;
     cs[i] = c;
     res = commLocalSetup(c);
+  }
+  if (res == ncclSuccess && ndev > 1) {
+    std::vector<SplitRecord> recs(ndev);
+    for (int i = 0; i < ndev; i++) recs[i] = makeSplitRecord(cs[i]);
+    for (int i = 0; i < ndev && res == ncclSuccess; i++) {
+      applySplits(cs[i], recs);
+      hipSetDevice(cs[i]->cudaDev);
+      res = transportPlan(cs[i]);
+    }
   }
   if (res == ncclSuccess && ndev > 1) {
     std::vector<std::vector<PeerOffsets>> tables(ndev);

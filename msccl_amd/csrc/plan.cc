@@ -53,6 +53,19 @@ bool mscclEnabled() {
   return listEnables(getenv("NCCL_ALGO"), "MSCCL", true);
 }
 
+int chooseSplit(int maxBlocks, int coResident) {
+  int64_t forced = envInt("MSCCL_AMD_SPLIT", 0);
+  int k = 1;
+  if (forced > 0) {
+    while (k * 2 <= kMaxSplit && k * 2 <= forced) k *= 2;
+    return k;
+  }
+  int64_t target = envInt("MSCCL_AMD_TARGET_WGS", 256);
+  int64_t per = (int64_t)std::max(1, maxBlocks) * std::max(1, coResident);
+  while (k * 2 <= kMaxSplit && per * k * 2 <= target) k *= 2;
+  return k;
+}
+
 bool protoEnabled(int proto) {
   static const char* names[3] = {"LL", "LL128", "Simple"};
   return listEnables(getenv("NCCL_PROTO"), names[proto], true);

@@ -49,6 +49,11 @@ bool inPlaceOf(int coll, const void* send, const void* recv, size_t count, int d
 int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c);
 // Fills *p; returns an ncclResult_t code.
 int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, Plan* p);
+// Workgroups per XML thread block for an algorithm whose largest rank program has maxBlocks
+// thread blocks when coResident ranks share a GPU: the largest power of two <= kMaxSplit that
+// keeps the GPU's workgroups within MSCCL_AMD_TARGET_WGS (default 256 = one per CU).
+// MSCCL_AMD_SPLIT forces a value.  Every rank must compute the same value.
+int chooseSplit(int maxBlocks, int coResident);
 // NCCL_ALGO / NCCL_PROTO gates
 bool mscclEnabled();
 bool protoEnabled(int proto);

@@ -70,10 +70,13 @@ ncclResult_t transportPlan(ncclComm* comm) {
   for (auto& kv : sends) { comm->sendKeys.push_back(kv.first); comm->sendProtoMask.push_back(kv.second); }
   for (auto& kv : recvs) { comm->recvKeys.push_back(kv.first); comm->recvProtoMask.push_back(kv.second); }
 
-  comm->table.assign((size_t)kMaxChannels * n, PeerOffsets{-1, -1, -1, -1});
+  const int S = comm->maxSplit;
+  const int64_t llBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->llSlotLines * 16, kFifoAlign);
+  const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
+  comm->table.assign((size_t)kMaxChannels * n, PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
   size_t off = 0;
-  for (auto& k : comm->sendKeys) { comm->table[(size_t)k.chan * n + k.peer].sendHead = (int64_t)off; off += kWordStride; }
-  for (auto& k : comm->recvKeys) { comm->table[(size_t)k.chan * n + k.peer].recvTail = (int64_t)off; off += kWordStride; }
+  for (auto& k : comm->sendKeys) { comm->table[(size_t)k.chan * n + k.peer].sendHead = (int64_t)off; off += kWordStride * S; }
+  for (auto& k : comm->recvKeys) { comm->table[(size_t)k.chan * n + k.peer].recvTail = (int64_t)off; off += kWordStride * S; }
   off = alignUp(off, kFifoAlign);
   for (size_t i = 0; i < comm->recvKeys.size(); i++) {
     auto& k = comm->recvKeys[i];
@@ -81,11 +84,11 @@ ncclResult_t transportPlan(ncclComm* comm) {
     // LL128 schedules run on the LL FIFO format in this build
     if (comm->recvProtoMask[i] & ((1u << kProtoLL) | (1u << kProtoLL128))) {
       po.recvLL = (int64_t)off;
-      off = alignUp(off + (size_t)kFifoSteps * comm->llSlotLines * 16, kFifoAlign);
+      off += (size_t)llBytes * S;
     }
     if (comm->recvProtoMask[i] & (1u << kProtoSimple)) {
       po.recvSimple = (int64_t)off;
-      off = alignUp(off + (size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
+      off += (size_t)simpleBytes * S;
     }
   }
   comm->arenaSize = off ? off : kFifoAlign;
@@ -102,9 +105,9 @@ ncclResult_t transportPlan(ncclComm* comm) {
 
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
                               const std::vector<char*>& peerBases) {
-  const int n = comm->nRanks, me = comm->rank;
-  std::vector<DevSendConn> hs(comm->sendKeys.size());
-  std::vector<DevRecvConn> hr(comm->recvKeys.size());
+  const int n = comm->nRanks, me = comm->rank, S = comm->maxSplit;
+  std::vector<DevSendConn> hs(comm->sendKeys.size() * S);
+  std::vector<DevRecvConn> hr(comm->recvKeys.size() * S);
   for (size_t i = 0; i < comm->sendKeys.size(); i++) {
     const ConnKey& k = comm->sendKeys[i];
     const PeerOffsets& theirs = tables[k.peer][(size_t)k.chan * n + me];
@@ -117,15 +120,17 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
       return ncclInvalidUsage;
     }
     char* pb = peerBases[k.peer];
-    DevSendConn& c = hs[i];
-    memset(&c, 0, sizeof(c));
-    c.ll = theirs.recvLL >= 0 ? (LLLine*)(pb + theirs.recvLL) : nullptr;
-    c.simple = theirs.recvSimple >= 0 ? pb + theirs.recvSimple : nullptr;
-    c.remoteTail = (uint64_t*)(pb + theirs.recvTail);
-    c.head = (uint64_t*)(comm->arena + mine.sendHead);
-    c.step = 0;
-    c.llSlotLines = comm->llSlotLines;
-    c.simpleSlotBytes = comm->simpleSlotBytes;
+    for (int s = 0; s < S; s++) {
+      DevSendConn& c = hs[i * S + s];
+      memset(&c, 0, sizeof(c));
+      c.ll = theirs.recvLL >= 0 ? (LLLine*)(pb + theirs.recvLL + s * theirs.llStride) : nullptr;
+      c.simple = theirs.recvSimple >= 0 ? pb + theirs.recvSimple + s * theirs.simpleStride : nullptr;
+      c.remoteTail = (uint64_t*)(pb + theirs.recvTail + s * theirs.wordStride);
+      c.head = (uint64_t*)(comm->arena + mine.sendHead + s * mine.wordStride);
+      c.step = 0;
+      c.llSlotLines = comm->llSlotLines;
+      c.simpleSlotBytes = comm->simpleSlotBytes;
+    }
   }
   for (size_t i = 0; i < comm->recvKeys.size(); i++) {
     const ConnKey& k = comm->recvKeys[i];
@@ -136,15 +141,17 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
            k.chan, k.peer);
       return ncclInvalidUsage;
     }
-    DevRecvConn& c = hr[i];
-    memset(&c, 0, sizeof(c));
-    c.ll = mine.recvLL >= 0 ? (LLLine*)(comm->arena + mine.recvLL) : nullptr;
-    c.simple = mine.recvSimple >= 0 ? comm->arena + mine.recvSimple : nullptr;
-    c.tail = (uint64_t*)(comm->arena + mine.recvTail);
-    c.remoteHead = (uint64_t*)(peerBases[k.peer] + theirs.sendHead);
-    c.step = 0;
-    c.llSlotLines = comm->llSlotLines;
-    c.simpleSlotBytes = comm->simpleSlotBytes;
+    for (int s = 0; s < S; s++) {
+      DevRecvConn& c = hr[i * S + s];
+      memset(&c, 0, sizeof(c));
+      c.ll = mine.recvLL >= 0 ? (LLLine*)(comm->arena + mine.recvLL + s * mine.llStride) : nullptr;
+      c.simple = mine.recvSimple >= 0 ? comm->arena + mine.recvSimple + s * mine.simpleStride : nullptr;
+      c.tail = (uint64_t*)(comm->arena + mine.recvTail + s * mine.wordStride);
+      c.remoteHead = (uint64_t*)(peerBases[k.peer] + theirs.sendHead + s * theirs.wordStride);
+      c.step = 0;
+      c.llSlotLines = comm->llSlotLines;
+      c.simpleSlotBytes = comm->simpleSlotBytes;
+    }
   }
   if (!hs.empty()) {
     if (hipMalloc(&comm->dSend, hs.size() * sizeof(DevSendConn)) != hipSuccess) return ncclUnhandledCudaError;

@@ -126,3 +126,13 @@ def test_golden_vectors_on_gpu(name):
     assert np.array_equal(np.stack(ins), z["inputs"])
     for r in range(n):
         assert np.array_equal(gpu[r].view(np.uint8), z["outputs"][r].view(np.uint8)), r
+
+
+@pytest.mark.parametrize("split", [1, 2, 8])
+@pytest.mark.parametrize("proto", ["LL", "Simple"])
+def test_workgroup_split_is_value_neutral(split, proto, monkeypatch):
+    """Running each XML thread block as `split` workgroups (sub-connections) changes no bit."""
+    monkeypatch.setenv("MSCCL_AMD_SPLIT", str(split))
+    check(xmlgen.allreduce_allpairs(4, 2, proto), 4, L.ALLREDUCE, 32 * 3001, 9)
+    check(xmlgen.allreduce_ring(4, 2, proto), 4, L.ALLREDUCE, 8 * 77, 7, op=2)
+    check(xmlgen.reduce_scatter_allpairs(4, 1, proto), 4, L.REDUCE_SCATTER, 4 * 1000 + 4, 6, inplace=False)
