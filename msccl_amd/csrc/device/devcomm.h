@@ -95,6 +95,7 @@ struct RankWork {
   int16_t refNthreads;          // reference nthreads (small-reduce switch, chunk rounding)
   uint8_t maxAllowedCount;
   uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
+  uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
 };
 
 struct LaunchArgs {

@@ -68,6 +68,7 @@ struct Interp {
   using F = Fn<T, OP>;
   static constexpr int TS = sizeof(T);
   static constexpr int PE = 16 / TS;  // elements per 16-B pack
+  static constexpr int U = 4;         // packs per lane per pass (memory-level parallelism)
 
   BlockShared* sh;
   DevComm* comm;
@@ -140,7 +141,7 @@ struct Interp {
 
   // ---------------------------------------------------------------- LL protocol
   template <int RECV, int SEND, int SRC, int DST>
-  __device__ void llOp(const T* src, T* dst, const Shape& s) {
+  __device__ void llOp(const T* src, T* dst, const Shape s) {
     constexpr int E = 8 / TS;  // elements per line
     const int nlinesFull = (s.n + E - 1) / E;
     if (SEND) waitSendCredit();
@@ -158,34 +159,60 @@ struct Interp {
     if (SRC) srs = makeRsrc(src);
     if (DST) drs = makeRsrc(dst);
     const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
-    for (int p = tid; p < s.npk; p += kNT) {
-      const int B = s.bufPack(p);
-      const int l0 = llLineIdx(p, 0), l1 = llLineIdx(p, 1);
-      const bool two = 2 * B + 1 < nlinesFull;
-      u32x4 data = {0, 0, 0, 0}, v;
-      if (SRC) data = loadPack(srs, vec, B, s.n);
+    // U packs per lane per pass: all their loads and line polls in flight together
+    for (int base = tid; base < s.npk; base += kNT * U) {
+      int B[U];
+      bool act[U], two[U];
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int p = base + u * kNT;
+        act[u] = p < s.npk;
+        B[u] = act[u] ? s.bufPack(p) : 0;
+        two[u] = act[u] && 2 * B[u] + 1 < nlinesFull;
+        v[u] = (u32x4){0, 0, 0, 0};
+      }
+      if (SRC) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (act[u]) v[u] = loadPack(srs, vec, B[u], s.n);
+      }
       if (RECV) {
-        u32x4 a, b = {0, 0, 0, 0};
-        uint32_t spins = 0;
-        if (two) {
-          do {
-            ldLines2(rslot + l0, rslot + l1, a, b);
-          } while ((a.y != rflag || a.w != rflag || b.y != rflag || b.w != rflag) && !spinAbort(spins));
-        } else {
-          do {
-            ldLine1(rslot + l0, a);
-          } while ((a.y != rflag || a.w != rflag) && !spinAbort(spins));
+        const void* la[2 * U];
+        u32x4 ln[2 * U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int p = base + u * kNT;
+          la[2 * u] = act[u] ? rslot + llLineIdx(p, 0) : rslot;
+          la[2 * u + 1] = two[u] ? rslot + llLineIdx(p, 1) : la[2 * u];
         }
-        u32x4 peer = {a.x, a.z, b.x, b.z};
-        v = SRC ? F::pack(peer, data) : peer;
-      } else {
-        v = data;
+        ldLines8(la, ln);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          uint32_t spins = 0;
+          while (act[u] && (ln[2 * u].y != rflag || ln[2 * u].w != rflag || ln[2 * u + 1].y != rflag ||
+                            ln[2 * u + 1].w != rflag)) {
+            if (spinAbort(spins)) break;
+            ldLines2(la[2 * u], la[2 * u + 1], ln[2 * u], ln[2 * u + 1]);
+          }
+          const u32x4 peer = {ln[2 * u].x, ln[2 * u].z, ln[2 * u + 1].x, ln[2 * u + 1].z};
+          v[u] = SRC ? F::pack(peer, v[u]) : peer;
+        }
       }
       if (SEND) {
-        st16<kAuxFifo>(frs, (uint32_t)l0 * 16, (u32x4){v.x, sflag, v.y, sflag});
-        if (two) st16<kAuxFifo>(frs, (uint32_t)l1 * 16, (u32x4){v.z, sflag, v.w, sflag});
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (!act[u]) continue;
+          const int p = base + u * kNT;
+          st16<kAuxFifo>(frs, (uint32_t)llLineIdx(p, 0) * 16, (u32x4){v[u].x, sflag, v[u].y, sflag});
+          if (two[u]) st16<kAuxFifo>(frs, (uint32_t)llLineIdx(p, 1) * 16, (u32x4){v[u].z, sflag, v[u].w, sflag});
+        }
       }
-      if (DST) storePack(drs, vec, B, s.n, v);
+      if (DST) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+          if (act[u]) storePack(drs, vec, B[u], s.n, v[u]);
+      }
     }
     if (SEND) {
       if ((sendStep & kLLCleanMask) == kLLCleanMask) {
@@ -207,7 +234,7 @@ struct Interp {
 
   // ---------------------------------------------------------------- Simple protocol
   template <int RECV, int SEND, int SRC, int DST>
-  __device__ void simpleOp(const T* src, T* dst, const Shape& s) {
+  __device__ void simpleOp(const T* src, T* dst, const Shape s) {
     const int slotBytes = SEND ? sc->simpleSlotBytes : rc->simpleSlotBytes;
     const int slicePacks = slotBytes / 16;
     __amdgpu_buffer_rsrc_t srs, drs, rrs, frs;
@@ -229,18 +256,35 @@ struct Interp {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
       if (SEND) frs = makeRsrc(sc->simple + (sendStep % kFifoSteps) * (uint64_t)slotBytes);
-      for (int p = s0 + tid; p < s1; p += kNT) {
-        const int B = s.bufPack(p);
-        u32x4 data = {0, 0, 0, 0}, v;
-        if (SRC) data = loadPack(srs, vec, B, s.n);
-        if (RECV) {
-          u32x4 peer = ld16<kAuxFifo>(rrs, (uint32_t)(p - s0) * 16);
-          v = SRC ? F::pack(data, peer) : peer;
-        } else {
-          v = data;
+      for (int base = s0 + tid; base < s1; base += kNT * U) {
+        int B[U];
+        bool act[U];
+        u32x4 v[U], peer[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          const int p = base + u * kNT;
+          act[u] = p < s1;
+          B[u] = act[u] ? s.bufPack(p) : 0;
+          v[u] = peer[u] = (u32x4){0, 0, 0, 0};
         }
-        if (SEND) st16<kAuxFifo>(frs, (uint32_t)(p - s0) * 16, v);
-        if (DST) storePack(drs, vec, B, s.n, v);
+        if (SRC) {
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (act[u]) v[u] = loadPack(srs, vec, B[u], s.n);
+        }
+        if (RECV) {
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            if (act[u]) peer[u] = ld16<kAuxFifo>(rrs, (uint32_t)(base + u * kNT - s0) * 16);
+#pragma unroll
+          for (int u = 0; u < U; u++) v[u] = SRC ? F::pack(v[u], peer[u]) : peer[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (!act[u]) continue;
+          if (SEND) st16<kAuxFifo>(frs, (uint32_t)(base + u * kNT - s0) * 16, v[u]);
+          if (DST) storePack(drs, vec, B[u], s.n, v[u]);
+        }
       }
       drainStores();
       __syncthreads();
@@ -254,64 +298,74 @@ struct Interp {
   }
 
   template <int RECV, int SEND, int SRC, int DST>
-  __device__ __forceinline__ void op(const T* src, T* dst, const Shape& s) {
+  __device__ __forceinline__ void op(const T* src, T* dst, const Shape s) {
     if constexpr (PROTO == pSimple) simpleOp<RECV, SEND, SRC, DST>(src, dst, s);
     else llOp<RECV, SEND, SRC, DST>(src, dst, s);
   }
 
   // ---------------------------------------------------------------- local ops
-  __device__ void localCopy(const T* src, T* dst, const Shape& s) {
+  __device__ void localCopy(const T* src, T* dst, const Shape s) {
     __amdgpu_buffer_rsrc_t srs = makeRsrc(src), drs = makeRsrc(dst);
     const bool vec = aligned16(src) && aligned16(dst);
-    for (int p = tid; p < s.npk; p += kNT) {
-      const int B = s.bufPack(p);
-      storePack(drs, vec, B, s.n, loadPack(srs, vec, B, s.n));
+    for (int base = tid; base < s.npk; base += kNT * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (base + u * kNT < s.npk) v[u] = loadPack(srs, vec, s.bufPack(base + u * kNT), s.n);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (base + u * kNT < s.npk) storePack(drs, vec, s.bufPack(base + u * kNT), s.n, v[u]);
     }
   }
 
-  // srcOffs[r]: element offsets of the reduction sources from srcBase (MSCCL_MAX_REDUCE_FUSION
-  // = 16).  The per-element path is chosen on the whole call's element count, as in the reference.
-  __device__ void reduce(const T* srcBase, const int64_t* srcOffs, int nsrc, T* dst, const Shape& s) {
+  // Source r of the fused reduction starts at srcBase + chunkOff + reds[r] * sizePer (reds: chunk
+  // indices in LDS, at most MSCCL_MAX_REDUCE_FUSION = 16).  The per-element path is chosen on the whole call's element count, as in the reference.
+  __device__ void reduce(const T* srcBase, const int16_t* reds, int64_t chunkOff, int64_t sizePer, int nsrc, T* dst,
+                         const Shape s) {
     if (s.n < refNthreads) {
       // per-element path, d first: o = fn(s_r, o) (msccl_interpreter.h:157-170)
-      __amdgpu_buffer_rsrc_t drs = makeRsrc(dst), srs = makeRsrc(srcBase);
+      __amdgpu_buffer_rsrc_t drs = makeRsrc(dst);
       for (int k = tid; k < s.npk * PE; k += kNT) {
         const int e = s.bufPack(k / PE) * PE + (k % PE);
         if (e >= s.n) continue;
         T o = ldElem<T>(drs, (uint32_t)e * TS);
-#pragma unroll
-        for (int r = 0; r < 16; r++)
-          if (r < nsrc) o = F::elem(ldElem<T>(srs, (uint32_t)(srcOffs[r] + e) * TS), o);
+        for (int r = 0; r < nsrc; r++)
+          o = F::elem(ldElem<T>(makeRsrc(srcBase + chunkOff + reds[r] * sizePer), (uint32_t)e * TS), o);
         stElem<T>(drs, (uint32_t)e * TS, o);
       }
       return;
     }
     __amdgpu_buffer_rsrc_t drs = makeRsrc(dst);
     bool vec = aligned16(dst);
+    for (int r = 0; r < nsrc; r++) vec = vec && aligned16(srcBase + chunkOff + reds[r] * sizePer);
+    for (int base = tid; base < s.npk; base += kNT * U) {
+      int B[U];
+      bool act[U];
+      u32x4 d[U], acc[U];
 #pragma unroll
-    for (int r = 0; r < 16; r++)
-      if (r < nsrc) vec = vec && aligned16(srcBase + srcOffs[r]);
-    for (int p = tid; p < s.npk; p += kNT) {
-      const int B = s.bufPack(p);
-      u32x4 d = loadPack(drs, vec, B, s.n);
-      u32x4 acc;
-      if constexpr (PROTO == pSimple) {
+      for (int u = 0; u < U; u++) {
+        act[u] = base + u * kNT < s.npk;
+        B[u] = act[u] ? s.bufPack(base + u * kNT) : 0;
+        d[u] = acc[u] = (u32x4){0, 0, 0, 0};
+        if (act[u]) d[u] = loadPack(drs, vec, B[u], s.n);
+      }
+      for (int r = 0; r < nsrc; r++) {
+        const __amdgpu_buffer_rsrc_t rs = makeRsrc(srcBase + chunkOff + reds[r] * sizePer);
+        u32x4 x[U];
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          if (r < nsrc) {
-            u32x4 x = loadPack(makeRsrc(srcBase + srcOffs[r]), vec, B, s.n);
-            acc = r == 0 ? x : F::pack(acc, x);
-          }
-        }
-        acc = F::pack(acc, d);
-      } else {
-        acc = d;
+        for (int u = 0; u < U; u++) x[u] = act[u] ? loadPack(rs, vec, B[u], s.n) : (u32x4){0, 0, 0, 0};
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          if (r < nsrc) acc = F::pack(acc, loadPack(makeRsrc(srcBase + srcOffs[r]), vec, B, s.n));
+        for (int u = 0; u < U; u++) {
+          if constexpr (PROTO == pSimple) acc[u] = r == 0 ? x[u] : F::pack(acc[u], x[u]);  // (s0(+)s1..)(+)d
+          else acc[u] = F::pack(r == 0 ? d[u] : acc[u], x[u]);                             // d(+)s0(+)s1..
         }
       }
-      storePack(drs, vec, B, s.n, acc);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (!act[u]) continue;
+        if constexpr (PROTO == pSimple) acc[u] = F::pack(acc[u], d[u]);
+        storePack(drs, vec, B[u], s.n, acc[u]);
+      }
     }
   }
 
@@ -354,7 +408,9 @@ struct Interp {
     uint64_t* flags = comm->flags;
     bool stop = false;
 
-    for (int64_t grid = 0, iter = 0; grid < sizePer && !stop; grid += chunkSize, iter++) {
+    const int64_t merge = w.merge;
+    int64_t nelemGrid = 0;
+    for (int64_t grid = 0, iter = 0; grid < sizePer && !stop; grid += nelemGrid, iter++) {
       int64_t real;
       if constexpr (PROTO == pSimple) {
         real = sizePer - grid < chunkSize ? sizePer - grid : chunkSize;
@@ -364,7 +420,13 @@ struct Interp {
         real = rem < chunkSize ? rem : chunkSize;
       }
       real = (int)real;
-      const int nelem = (int)(real < sizePer - grid ? real : sizePer - grid);
+      int nelem = (int)(real < sizePer - grid ? real : sizePer - grid);
+      if (nelem == chunkSize && merge > 1) {
+        // run up to `merge` consecutive full iterations as one (enqueue.cc: makeWork)
+        const int64_t full = (sizePer - grid) / chunkSize;
+        nelem = (int)(chunkSize * (full < merge ? full : merge));
+      }
+      nelemGrid = nelem;
       // this workgroup's positions inside every chunk of this iteration (nelem % PE == 0
       // whenever split > 1: the host sets split = 1 otherwise)
       const int Qc = (nelem + PE - 1) / PE;
@@ -415,11 +477,7 @@ struct Interp {
             case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
             case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
             case tRe: {
-              int64_t offs[16];
-#pragma unroll
-              for (int r = 0; r < 16; r++)
-                offs[r] = r < t.numReds ? grid + (int64_t)(sh->red[t.redPtr + r] + c) * sizePer : 0;
-              reduce(srcP, offs, t.numReds, dstP + dstoff, s);
+              reduce(srcP, sh->red + t.redPtr, grid + (int64_t)c * sizePer, sizePer, t.numReds, dstP + dstoff, s);
               if (c == 0) step += t.numReds - 1;
               __syncthreads();
               break;

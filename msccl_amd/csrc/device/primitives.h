@@ -90,6 +90,22 @@ __device__ __forceinline__ void ldLines2(const void* a, const void* b, u32x4& x,
       : "v"(a), "v"(b)
       : "memory");
 }
+// Eight FIFO lines (four packs) in flight, one wait.
+__device__ __forceinline__ void ldLines8(const void* const* p, u32x4* x) {
+  asm volatile(
+      "global_load_dwordx4 %0, %8, off sc0 sc1\n\t"
+      "global_load_dwordx4 %1, %9, off sc0 sc1\n\t"
+      "global_load_dwordx4 %2, %10, off sc0 sc1\n\t"
+      "global_load_dwordx4 %3, %11, off sc0 sc1\n\t"
+      "global_load_dwordx4 %4, %12, off sc0 sc1\n\t"
+      "global_load_dwordx4 %5, %13, off sc0 sc1\n\t"
+      "global_load_dwordx4 %6, %14, off sc0 sc1\n\t"
+      "global_load_dwordx4 %7, %15, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
 __device__ __forceinline__ void ldLine1(const void* a, u32x4& x) {
   asm volatile(
       "global_load_dwordx4 %0, %1, off sc0 sc1\n\t"

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 #include <thread>
 #include <vector>
@@ -110,6 +111,19 @@ RankWork makeWork(Planned& p) {
   if (p.plan.sizePerChunk % (16 / refTypeSize(p.plan.dtype)) != 0) split = 1;
   w.split = (uint8_t)split;
   w.nBlocks = (int16_t)(da.nBlocks * split);
+  // Consecutive full interpreter iterations can run as one: every element still sees the same
+  // operations in the same order (only a partial last iteration can take the per-element reduce
+  // path, and it stays an iteration of its own).  An LL step of a sub-connection must still fit
+  // one FIFO slot, so at most `split` LL iterations merge.  maxAllowedCount is 1 whenever there
+  // is more than one iteration, so one op never exceeds M chunks.
+  int merge = 1;
+  if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {
+    const int64_t envMerge = envInt("MSCCL_AMD_MERGE", 0);
+    merge = envMerge > 0 ? (int)envMerge : (p.plan.proto == kProtoSimple ? 4 : split);
+    if (p.plan.proto != kProtoSimple) merge = std::min(merge, split);
+    merge = std::max(1, std::min(merge, 64));
+  }
+  w.merge = (uint8_t)merge;
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.workIndex = comm->workIndex++;

@@ -92,7 +92,9 @@ ncclResult_t transportPlan(ncclComm* comm) {
     }
   }
   comm->arenaSize = off ? off : kFifoAlign;
-  hipError_t e = hipExtMallocWithFlags((void**)&comm->arena, comm->arenaSize, hipDeviceMallocUncached);
+  hipError_t e = envInt("MSCCL_AMD_ARENA_COARSE", 0)
+                     ? hipMalloc((void**)&comm->arena, comm->arenaSize)
+                     : hipExtMallocWithFlags((void**)&comm->arena, comm->arenaSize, hipDeviceMallocUncached);
   if (e != hipSuccess) {
     WARN("MSCCL: cannot allocate %zu bytes of uncached transport memory: %s", comm->arenaSize, hipGetErrorString(e));
     return ncclUnhandledCudaError;
