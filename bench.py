@@ -121,6 +121,30 @@ def cpu_baseline(n: int, nbytes: int, dt: int, seconds: float):
             "ms_per_allreduce": round(t * 1e3, 4)}
 
 
+def workload_desc(multi: bool, n: int, proto: str, dtname: str) -> str:
+    if not multi:
+        return ("C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
+                "(fused launch, local HBM in place of xGMI)" % (n, proto, dtname))
+    return ("%s: %d-rank all-pairs %s AllReduce over xGMI, %s, one rank per GPU"
+            % ("C3" if n == 8 else "C2-family", n, proto, dtname))
+
+
+def pmc_traffic(cfg_key: dict):
+    """HBM bytes per headline launch from the committed rocprofv3 PMC summary of the same
+    configuration (tools/profile.sh -> profiles/<tag>_pmc.json), or (None, None)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
+        try:
+            pmc = json.load(open(f))
+            bench = json.load(open(f.replace("_pmc.json", "_bench.json")))
+        except (OSError, ValueError):
+            continue
+        c = bench.get("config", {})
+        if all(c.get(k, {} if k == "knobs" else None) == v for k, v in cfg_key.items()) and pmc.get("traffic_bytes_per_launch"):
+            return round(pmc["traffic_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def main():
     a = parse()
     import torch
@@ -223,6 +247,10 @@ def main():
         link = XGMI_LINK_GBS * (n - 1)
         roof["xgmi"] = {"busbw": head["busbw"], "peak": link, "frac": round(head["busbw"] / link, 4),
                         "ll_ceiling": round(link * (0.5 if proto_id == 0 else 1.0), 1)}
+    workload = workload_desc(multi, n, a.proto, dtname)
+    knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("MSCCL_AMD_") and k != "MSCCL_AMD_TIMEOUT_SEC"}
+    cfg_key = {"workload": workload, "bytes_per_rank": head["bytes"], "instances_large": inst, "knobs": knobs}
+    roof["traffic"], roof["traffic_source"] = pmc_traffic(cfg_key)
     e2e = None
     if a.e2e and rank == 0 and not multi:
         e2e = measure_e2e(comms, n, maxb, dt, ts, stream, devs[0])
@@ -235,12 +263,10 @@ def main():
         "warmup": a.warmup, "ms_per_step": head["ms"], "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}.get(dtname, dtname),
         "data": "synthetic",
-        "config": {"workload": ("C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
-                                "(fused launch, local HBM in place of xGMI)" % (n, a.proto, dtname)) if not multi
-                   else ("%s: %d-rank all-pairs %s AllReduce over xGMI, %s, one rank per GPU"
-                         % ("C3" if n == 8 else "C2-family", n, a.proto, dtname)),
+        "config": {"workload": workload,
                    "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
-                   "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]]},
+                   "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
+                   "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -108,7 +108,12 @@ RankWork makeWork(Planned& p) {
   // Workgroups of a split thread block own 16-B pack positions inside each chunk, so a split
   // needs whole packs per chunk; sizePerChunk is identical on every rank, so all ranks agree.
   int split = comm->algoSplit.empty() ? 1 : comm->algoSplit[p.plan.algoIndex];
-  if (p.plan.sizePerChunk % (16 / refTypeSize(p.plan.dtype)) != 0) split = 1;
+  const int64_t pe = 16 / refTypeSize(p.plan.dtype);
+  if (p.plan.sizePerChunk % pe != 0) split = 1;
+  // Small messages: fewer, fuller workgroups (at least one pack per lane of every workgroup);
+  // a split forced with MSCCL_AMD_SPLIT is kept as is.
+  if (envInt("MSCCL_AMD_SPLIT", 0) <= 0)
+    while (split > 1 && p.plan.sizePerChunk / pe < (int64_t)split * kNT) split /= 2;
   w.split = (uint8_t)split;
   w.nBlocks = (int16_t)(da.nBlocks * split);
   // Consecutive full interpreter iterations can run as one: every element still sees the same

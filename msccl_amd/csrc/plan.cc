@@ -60,7 +60,7 @@ int chooseSplit(int maxBlocks, int coResident) {
     while (k * 2 <= kMaxSplit && k * 2 <= forced) k *= 2;
     return k;
   }
-  int64_t target = envInt("MSCCL_AMD_TARGET_WGS", 256);
+  int64_t target = envInt("MSCCL_AMD_TARGET_WGS", 512);
   int64_t per = (int64_t)std::max(1, maxBlocks) * std::max(1, coResident);
   while (k * 2 <= kMaxSplit && per * k * 2 <= target) k *= 2;
   return k;

@@ -136,3 +136,16 @@ def test_workgroup_split_is_value_neutral(split, proto, monkeypatch):
     check(xmlgen.allreduce_allpairs(4, 2, proto), 4, L.ALLREDUCE, 32 * 3001, 9)
     check(xmlgen.allreduce_ring(4, 2, proto), 4, L.ALLREDUCE, 8 * 77, 7, op=2)
     check(xmlgen.reduce_scatter_allpairs(4, 1, proto), 4, L.REDUCE_SCATTER, 4 * 1000 + 4, 6, inplace=False)
+
+
+@pytest.mark.parametrize("proto,per_chunk,dt", [
+    ("LL", 8192 * 3 + 100, 7),        # 3 full LL iterations (merged) + a partial one on the per-element path
+    ("LL", 8192 * 5, 9),              # bf16: 2.5 LL iterations
+    ("Simple", 524288 * 2 + 1000, 7),  # 2 full Simple iterations (merged) + a partial one
+])
+def test_merged_iterations_are_value_neutral(proto, per_chunk, dt):
+    """Consecutive full interpreter iterations run as one op (RankWork.merge): bit-exact vs the
+    oracle, which runs the reference's iteration grid one iteration at a time."""
+    x = xmlgen.allreduce_allpairs(2, 1, proto)
+    ncpl = 4
+    check(x, 2, L.ALLREDUCE, ncpl * per_chunk, dt)

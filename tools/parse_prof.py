@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Summarise a tools/profile.sh run into profiles/<tag>_*.
+
+Reads rocprofv3 CSVs (kernel stats, kernel trace, FETCH_SIZE and WRITE_SIZE counter passes) and
+writes:
+  profiles/<tag>_kernel_stats.csv   the --stats summary as rocprofv3 wrote it
+  profiles/<tag>_pmc.json           per-launch averages for the MSCCL kernel: duration (trace),
+                                    FETCH_SIZE, WRITE_SIZE and the HBM traffic they imply
+                                    (FETCH_SIZE doubled: on gfx950 it reports half the bytes of a
+                                    16-B/lane streaming read, MI355X_MICROARCH.md "HBM"; both in KiB)
+  profiles/<tag>_bench.json         the bench JSON line printed under the kernel-trace pass
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+
+def rows(path):
+    with open(path, newline="") as f:
+        return list(csv.DictReader(f))
+
+
+def col(row, *names):
+    low = {k.lower(): k for k in row}
+    for n in names:
+        if n.lower() in low:
+            return row[low[n.lower()]]
+    raise KeyError(names)
+
+
+def find(d, pattern):
+    return sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+
+
+def is_msccl(name):
+    return "mscclKernel" in name
+
+
+def counter_avg(d, counter):
+    files = find(d, "*counter_collection.csv")
+    vals = []
+    for f in files:
+        for r in rows(f):
+            if not is_msccl(col(r, "Kernel_Name", "KernelName", "Kernel-Name")):
+                continue
+            if col(r, "Counter_Name", "CounterName") != counter:
+                continue
+            vals.append(float(col(r, "Counter_Value", "CounterValue")))
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def main():
+    out, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    res = {"tag": tag}
+    stats = find(os.path.join(out, "kt"), "*kernel_stats.csv")
+    if stats:
+        shutil.copy(stats[0], os.path.join(prof, tag + "_kernel_stats.csv"))
+        for r in rows(stats[0]):
+            if is_msccl(col(r, "Name", "KernelName", "Kernel_Name")):
+                res["kernel"] = col(r, "Name", "KernelName", "Kernel_Name")
+                res["stats_calls"] = int(col(r, "Calls"))
+                res["stats_avg_ns"] = float(col(r, "AverageNs", "Average_Ns", "AvgNs"))
+    traces = find(os.path.join(out, "kt"), "*kernel_trace.csv")
+    durs = []
+    for f in traces:
+        for r in rows(f):
+            if is_msccl(col(r, "Kernel_Name", "KernelName")):
+                durs.append(int(col(r, "End_Timestamp", "EndNs")) - int(col(r, "Start_Timestamp", "BeginNs")))
+    if durs:
+        res["trace_launches"] = len(durs)
+        res["trace_avg_ns"] = sum(durs) / len(durs)
+    fetch, nf = counter_avg(os.path.join(out, "fetch"), "FETCH_SIZE")
+    write, nw = counter_avg(os.path.join(out, "write"), "WRITE_SIZE")
+    res["fetch_size_kib_avg"], res["fetch_launches"] = fetch, nf
+    res["write_size_kib_avg"], res["write_launches"] = write, nw
+    if fetch is not None and write is not None:
+        res["traffic_bytes_per_launch"] = (2.0 * fetch + write) * 1024.0
+        res["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 per mscclKernel dispatch (gfx950 FETCH_SIZE correction)"
+    kt = os.path.join(out, "kt.json")
+    if os.path.exists(kt):
+        try:
+            line = [ln for ln in open(kt).read().splitlines() if ln.startswith("{")][-1]
+            bench = json.loads(line)
+            json.dump(bench, open(os.path.join(prof, tag + "_bench.json"), "w"), indent=1)
+            res["bench_kernel_ms"] = bench["roofline"].get("kernel_ms")
+            res["bench_algorithmic_bytes_per_launch"] = bench["roofline"].get("algorithmic_bytes_per_launch")
+        except (IndexError, ValueError, KeyError):
+            pass
+    json.dump(res, open(os.path.join(prof, tag + "_pmc.json"), "w"), indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
