@@ -10,9 +10,10 @@
 //   * a launch may carry the work of several co-resident ranks (ranks that share one GPU):
 //     RankWork[i] owns blocks [blockBase, blockBase + nBlocks);
 //   * one XML thread block may run as `split` workgroups: workgroup k of a tb owns the k-th
-//     1/split of the 16-B packs of every primitive call and its own sub-connection (FIFO,
-//     head/tail words, step counter) and dependency flag, so the values produced are the
-//     same as with one workgroup (the split is by element, every element keeps its order).
+//     1/split of the 16-B packs of every MSCCL chunk (by position inside the chunk) and its own
+//     sub-connection (FIFO, head/tail words, step counter) and dependency flag, so the values
+//     produced are the same as with one workgroup (the split is by element, every element
+//     keeps its operations and their order).
 #pragma once
 #include <stdint.h>
 

@@ -5,6 +5,8 @@ import os
 import re
 import subprocess
 
+import pytest
+
 import msccl_amd as M
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -56,3 +58,27 @@ def test_enum_values_match_reference():
                       ("ncclUint64", 5), ("ncclFloat16", 6), ("ncclFloat32", 7), ("ncclFloat64", 8),
                       ("ncclBfloat16", 9), ("ncclInvalidUsage", 5), ("ncclUnhandledCudaError", 1)]:
         assert re.search(r"\b%s\s*=\s*%d\b" % (name, val), hdr), name
+
+
+def build_c_example(tmp_path):
+    """Compile examples/c_allreduce.c against include/nccl.h + libmsccl_amd.so (a C caller written
+    for the reference header, as nccl-tests is)."""
+    import shutil
+    import subprocess
+    if not shutil.which("gcc"):
+        pytest.skip("gcc missing")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "c_allreduce")
+    cmd = ["gcc", "-O2", "-Wall", "-Werror", "-I" + os.path.join(root, "include"), "-I/opt/rocm/include",
+           "-D__HIP_PLATFORM_AMD__", os.path.join(root, "examples", "c_allreduce.c"), "-o", exe,
+           "-L" + os.path.join(root, "msccl_amd"), "-lmsccl_amd", "-L/opt/rocm/lib", "-lamdhip64",
+           "-Wl,-rpath," + os.path.join(root, "msccl_amd"), "-Wl,-rpath,/opt/rocm/lib"]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return exe
+
+
+def test_c_caller_compiles_and_links(tmp_path):
+    import subprocess
+    exe = build_c_example(tmp_path)
+    out = subprocess.run([exe, "2", "16", "--version-only"], check=True, capture_output=True, text=True).stdout
+    assert "21212" in out

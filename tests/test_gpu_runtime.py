@@ -165,3 +165,16 @@ def test_stream_ordering_separate_streams():
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_c_caller_allreduce(tmp_path):
+    """examples/c_allreduce.c (compiled against include/nccl.h) runs a 2-rank grouped AllReduce."""
+    import subprocess
+    from tests.test_abi import build_c_example
+    from msccl_amd import xmlgen
+    exe = build_c_example(tmp_path)
+    xml = tmp_path / "ap2.xml"
+    xml.write_text(xmlgen.allreduce_allpairs(2, 2, "LL"))
+    env = dict(os.environ, MSCCL_XML_FILES=str(xml), MSCCL_AMD_TIMEOUT_SEC="20")
+    r = subprocess.run([exe, "2", str(8 * 40000)], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
