@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", help="also time H2D + AllReduce + D2H")
+    ap.add_argument("--graph", action="store_true", help="time the K steps as one captured hipGraph replay")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -182,7 +183,8 @@ def main():
         if multi:
             torch.distributed.barrier()
 
-    stream = torch.cuda.current_stream(devs[0])
+    stream = torch.cuda.Stream(devs[0])
+    stream.wait_stream(torch.cuda.current_stream(devs[0]))
     maxb = max(sizes)
     bufs = [torch.empty(maxb // 4 + 64, dtype=torch.float32, device=d).uniform_(-1, 1) for d in devs]
     algo_large = M.algo_json(xmls[1], my_ranks[0], n)
@@ -203,12 +205,24 @@ def main():
             continue
         for _ in range(a.warmup):
             one_step(nbytes)
+        graph = None
+        if a.graph:
+            # nccl-tests -G style: the K timed steps captured once into a hipGraph, replayed once
+            torch.cuda.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+                for _ in range(a.steps):
+                    one_step(nbytes)
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record(stream)
-        for _ in range(a.steps):
-            one_step(nbytes)
+        if graph is not None:
+            with torch.cuda.stream(stream):
+                graph.replay()
+        else:
+            for _ in range(a.steps):
+                one_step(nbytes)
         ev1.record(stream)
         torch.cuda.synchronize()
         barrier()
@@ -266,11 +280,12 @@ def main():
         "config": {"workload": workload,
                    "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
+                   "launch": "hipgraph" if a.graph else "eager",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
         "roofline": roof,
         "cpu_baseline": cpu,
-        "sweep": [{k: r[k] for k in ("bytes", "ms", "busbw")} for r in results],
+        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw")} for r in results],
     }
     if e2e:
         out["e2e"] = e2e

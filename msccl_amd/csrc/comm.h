@@ -72,8 +72,7 @@ struct ncclComm {
   uint64_t* dFlags = nullptr;
   void* scratch = nullptr;
   size_t scratchSize = 0;
-  uint32_t workIndex = 1;
-  bool flagsNeedReset = false;
+  uint32_t workIndex = 1;    // host launch counter (the device epoch drives the flags)
   msccl::DevComm* dComm = nullptr;
 
   // failure handling
@@ -104,7 +103,7 @@ bool commValid(const ncclComm* comm);
 // transport.cc
 ncclResult_t transportPlan(ncclComm* comm);                 // keys, arena layout, allocation, own table
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
-                              const std::vector<char*>& peerBases);
+                              const std::vector<char*>& peerBases, const std::vector<int>& peerRemote);
 ncclResult_t algoUpload(ncclComm* comm);
 
 // enqueue.cc

@@ -25,6 +25,7 @@ constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag
 constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
 constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kMaxSplit
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
+constexpr int kCounterWords = 16;      // uint64 words per launch counter (own 128-B line)
 
 // LL FIFO line (ncclLLFifoLine, devcomm.h:35-48): two 8-B {4-B data, 4-B flag} granules.
 struct alignas(16) LLLine { uint32_t d0, f0, d1, f1; };
@@ -55,6 +56,8 @@ struct DevSendConn {
   uint64_t step;                // persistent step counter (owned by one workgroup)
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
+  int32_t remote;               // receiver on another GPU: system-scope release before a tail post
+  int32_t pad;
 };
 
 struct DevRecvConn {
@@ -76,6 +79,11 @@ struct DevComm {
   uint64_t timeoutTicks;        // s_memrealtime ticks (100 MHz)
   int32_t maxSplit;             // sub-connections per (channel, peer): conn k of key c = send[c*maxSplit+k]
   int32_t pad;
+  // Launch epoch (the reference's host-side workIndex, enqueue.cc:714-721, kept on the device so
+  // that a captured hipGraph replays correctly): every workgroup of a launch reads *epoch at
+  // start; the last workgroup to finish (counted in *done) advances it for the next launch.
+  uint64_t* epoch;
+  uint32_t* done;
 };
 
 // One rank's share of a launch (the reference passes ncclDevComm* + a 64-B ncclWorkElem,
@@ -90,7 +98,7 @@ struct RankWork {
   int64_t sizePerChunk;         // sizePerMscclChunk = count*sizeMultiplier/nchunksPerLoop (elements)
   int64_t chunkSize;            // interpreter chunkSize (elements)
   int64_t minChunk;             // LL: nthreads*8/sizeof(T); Simple: rounding unit (nthreads-32)*8/sizeof(T)
-  uint32_t workIndex;
+  uint32_t launchSeq;            // host launch counter (diagnostics only; flags use DevComm::epoch)
   int16_t blockBase;
   int16_t nBlocks;              // workgroups = XML thread blocks x split
   int16_t refNthreads;          // reference nthreads (small-reduce switch, chunk rounding)

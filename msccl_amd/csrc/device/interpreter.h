@@ -37,6 +37,7 @@ struct alignas(16) BlockShared {
   int16_t depStep[256];
   int16_t red[256];
   uint64_t step[2];
+  uint64_t epoch;
   uint32_t aborted;
 };
 
@@ -289,6 +290,12 @@ struct Interp {
       drainStores();
       __syncthreads();
       if (tid == 0) {
+        if (SEND && sc->remote) {
+          // FIFO bytes went to another GPU: system-scope release before the tail (the reference's
+          // __threadfence_system before postPeer, prims_simple.h:218)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          drainStores();
+        }
         if (SEND) atomicStoreSys(sc->remoteTail, sendStep + 1);
         if (RECV) atomicStoreSys(rc->remoteHead, recvStep + 1);
       }
@@ -393,6 +400,7 @@ struct Interp {
       sh->step[0] = sc ? sc->step : 0;
       sh->step[1] = rc ? rc->step : 0;
       sh->aborted = 0;
+      sh->epoch = atomicLoadAgent(comm->epoch);
     }
     __syncthreads();
     sendStep = sh->step[0];
@@ -404,7 +412,7 @@ struct Interp {
     const int64_t sizePer = w.sizePerChunk;
     const int64_t chunkSize = w.chunkSize;
     const int mac = w.maxAllowedCount;
-    const uint64_t workIndex = w.workIndex;
+    const uint64_t workIndex = sh->epoch;  // COMPUTE_FLAG's workIndex (msccl_interpreter.h:14-16)
     uint64_t* flags = comm->flags;
     bool stop = false;
 
@@ -500,6 +508,11 @@ struct Interp {
     if (tid == 0) {
       if (sc) sc->step = sendStep;
       if (rc) rc->step = recvStep;
+      // the last workgroup of this rank's launch advances the epoch for the next launch
+      if (__hip_atomic_fetch_add(comm->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)w.nBlocks - 1) {
+        __hip_atomic_store(comm->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicStoreAgent(comm->epoch, workIndex + 1);
+      }
     }
   }
 };

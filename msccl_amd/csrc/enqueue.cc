@@ -131,9 +131,7 @@ RankWork makeWork(Planned& p) {
   w.merge = (uint8_t)merge;
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
-  w.workIndex = comm->workIndex++;
-  // flag reset when workIndex approaches overflow (enqueue.cc:714-721)
-  if (comm->flagsNeedReset || comm->workIndex > 0xFFFFFFFFu - 4096u) comm->flagsNeedReset = true;
+  w.launchSeq = comm->workIndex++;
   return w;
 }
 
@@ -144,13 +142,11 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   LaunchArgs args;
   memset(&args, 0, sizeof(args));
   int blocks = 0;
-  std::vector<ncclComm*> resets;
   for (size_t i = 0; i < ps.size(); i++) {
     RankWork w = makeWork(*ps[i]);
     w.blockBase = (int16_t)blocks;
     blocks += w.nBlocks;
     args.w[i] = w;
-    if (ps[i]->op.comm->flagsNeedReset) resets.push_back(ps[i]->op.comm);
   }
   args.nRanks = (int)ps.size();
   if (blocks == 0) return ncclSuccess;
@@ -162,11 +158,6 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
       hipEventRecord(e, ps[i]->op.stream);
       hipStreamWaitEvent(primary, e, 0);
     }
-  }
-  for (ncclComm* c : resets) {
-    hipMemsetAsync(c->dFlags, 0, (size_t)kFlagSlots * kFlagStride * sizeof(uint64_t), primary);
-    c->workIndex = 1;
-    c->flagsNeedReset = false;
   }
   const Planned& p0 = *ps[0];
   LaunchFn fn = getLaunchFn(p0.plan.dtype, p0.op.op, p0.plan.proto);

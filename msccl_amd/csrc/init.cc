@@ -51,8 +51,13 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
   *comm->hostErr = 0;
   NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devAbort, comm->hostAbort, 0), "hipHostGetDevicePointer"));
   NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devErr, comm->hostErr, 0), "hipHostGetDevicePointer"));
-  NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, (size_t)kFlagSlots * kFlagStride * sizeof(uint64_t)), "hipMalloc flags"));
-  NCCLCHECK(hipErr(hipMemset(comm->dFlags, 0, (size_t)kFlagSlots * kFlagStride * sizeof(uint64_t)), "hipMemset"));
+  // flags, then the launch epoch and the done counter on lines of their own
+  const size_t flagWords = (size_t)kFlagSlots * kFlagStride + 2 * kCounterWords;
+  NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, flagWords * sizeof(uint64_t)), "hipMalloc flags"));
+  NCCLCHECK(hipErr(hipMemset(comm->dFlags, 0, flagWords * sizeof(uint64_t)), "hipMemset"));
+  const uint64_t epoch0 = 1;  // flags start at 0, the first launch waits for epoch 1 (init.cc:300-302)
+  NCCLCHECK(hipErr(hipMemcpy(comm->dFlags + (size_t)kFlagSlots * kFlagStride, &epoch0, sizeof(epoch0),
+                             hipMemcpyHostToDevice), "hipMemcpy epoch"));
   comm->workIndex = 1;  // flags start at 0 (init.cc:300-302)
   NCCLCHECK(hipErr(hipEventCreateWithFlags(&comm->doneEvent, hipEventDisableTiming), "hipEventCreate"));
   // scratch = max over algorithms of maxBytes * s_chunks / nchunksperloop (init.cc:809-835)
@@ -129,6 +134,8 @@ ncclResult_t commFinish(ncclComm* comm) {
   dc.errWord = comm->devErr;
   dc.timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
   dc.maxSplit = comm->maxSplit;
+  dc.epoch = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  dc.done = (uint32_t*)(dc.epoch + kCounterWords);
   NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
   NCCLCHECK(hipErr(hipMemcpy(comm->dComm, &dc, sizeof(dc), hipMemcpyHostToDevice), "hipMemcpy"));
   NCCLCHECK(hipErr(hipDeviceSynchronize(), "hipDeviceSynchronize"));
@@ -173,6 +180,10 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
     std::vector<std::vector<PeerOffsets>> tables(n);
     comm->peerArena.assign(n, nullptr);
     comm->peerArenaIpc.assign(n, false);
+    // a peer is remote (xGMI) unless it runs on the same GPU: same host and PCI bus id
+    std::vector<int> peerRemote(n, 0);
+    for (int r = 0; r < n; r++)
+      peerRemote[r] = strcmp(recs[r].host, srec.host) != 0 || strcmp(recs[r].bus, srec.bus) != 0;
     for (int r = 0; r < n; r++) {
       tables[r].resize(comm->table.size());
       memcpy(tables[r].data(), tall.data() + (size_t)r * tbytes, tbytes);
@@ -194,7 +205,7 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
         comm->peerArenaIpc[r] = true;
       }
     }
-    NCCLCHECK(transportConnect(comm, tables, comm->peerArena));
+    NCCLCHECK(transportConnect(comm, tables, comm->peerArena, peerRemote));
   }
   NCCLCHECK(commFinish(comm));
   NCCLCHECK(sb->barrier());
@@ -325,9 +336,11 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
           (void)hipGetLastError();
         }
       }
+      std::vector<int> remote(ndev);
+      for (int j = 0; j < ndev; j++) remote[j] = cs[j]->cudaDev != cs[i]->cudaDev;
       cs[i]->peerArena = bases;
       cs[i]->peerArenaIpc.assign(ndev, false);
-      if (res == ncclSuccess) res = transportConnect(cs[i], tables, bases);
+      if (res == ncclSuccess) res = transportConnect(cs[i], tables, bases, remote);
     }
   }
   for (int i = 0; i < ndev && res == ncclSuccess; i++) {

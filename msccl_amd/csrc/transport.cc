@@ -106,7 +106,7 @@ ncclResult_t transportPlan(ncclComm* comm) {
 }
 
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
-                              const std::vector<char*>& peerBases) {
+                              const std::vector<char*>& peerBases, const std::vector<int>& peerRemote) {
   const int n = comm->nRanks, me = comm->rank, S = comm->maxSplit;
   std::vector<DevSendConn> hs(comm->sendKeys.size() * S);
   std::vector<DevRecvConn> hr(comm->recvKeys.size() * S);
@@ -132,6 +132,7 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
       c.step = 0;
       c.llSlotLines = comm->llSlotLines;
       c.simpleSlotBytes = comm->simpleSlotBytes;
+      c.remote = peerRemote[k.peer];
     }
   }
   for (size_t i = 0; i < comm->recvKeys.size(); i++) {

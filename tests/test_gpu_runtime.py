@@ -178,3 +178,55 @@ def test_c_caller_allreduce(tmp_path):
     env = dict(os.environ, MSCCL_XML_FILES=str(xml), MSCCL_AMD_TIMEOUT_SEC="20")
     r = subprocess.run([exe, "2", str(8 * 40000)], env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("proto", ["LL", "Simple"])
+def test_hip_graph_capture_and_replay(proto, tmp_path):
+    """A grouped AllReduce captured into a hipGraph replays correctly: the launch epoch that
+    drives the dependency flags lives on the device (DevComm::epoch), not in the captured
+    arguments."""
+    import torch
+    import msccl_amd as M
+    from msccl_amd import xmlgen
+    xml = tmp_path / "ap.xml"
+    xml.write_text(xmlgen.allreduce_allpairs(2, 2, proto))
+    os.environ["MSCCL_XML_FILES"] = str(xml)
+    n, count = 2, 8 * 5000
+    comms = M.Comm.init_all([0] * n)
+    try:
+        g = torch.Generator().manual_seed(3)
+        init = [torch.randint(-4, 5, (count,), generator=g).float() for _ in range(n)]
+        bufs = [t.cuda() for t in init]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+
+        def step():
+            with M.group():
+                for c, b in zip(comms, bufs):
+                    c.all_reduce(b.data_ptr(), b.data_ptr(), count, M.FLOAT32, M.SUM, s.cuda_stream)
+
+        with torch.cuda.stream(s):
+            step()  # eager warm-up launch (epoch 1)
+        torch.cuda.synchronize()
+        expect = init[0] + init[1]
+        for b in bufs:
+            assert torch.equal(b.cpu(), expect)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=s, capture_error_mode="relaxed"):
+            step()
+        for k in range(6):
+            graph.replay()
+            torch.cuda.synchronize()
+            expect = expect * 2
+            for b in bufs:
+                assert torch.equal(b.cpu(), expect), k
+        step()  # eager again after replays
+        torch.cuda.synchronize()
+        expect = expect * 2
+        for b in bufs:
+            assert torch.equal(b.cpu(), expect)
+        for c in comms:
+            assert c.async_error() == 0
+    finally:
+        for c in comms:
+            c.destroy()
