@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", help="also time H2D + AllReduce + D2H")
     ap.add_argument("--graph", action="store_true", help="time the K steps as one captured hipGraph replay")
+    ap.add_argument("--extras", default=None,
+                    help="also measure C4 (ring Simple bf16 256 MiB) / C5 (RS+AG fp32 64 MiB), e.g. C4,C5 "
+                         "(default: both when 8 ranks run one per GPU)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -146,6 +149,105 @@ def pmc_traffic(cfg_key: dict):
     return None, None
 
 
+def init_comms(multi: bool, world: int, rank: int, n: int):
+    """Communicators for the current MSCCL_XML_FILES: one per process (multi) or n co-resident."""
+    if multi:
+        import torch.distributed as dist
+        obj = [M.get_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        return [M.Comm.init_rank(world, obj[0], rank)]
+    return M.Comm.init_all([0] * n)
+
+
+def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str) -> dict:
+    """BASELINE.json configs[3] (C4: ring AllReduce, Simple, bf16, 256 MiB per rank) and
+    configs[4] (C5: all-pairs ReduceScatter then AllGather, fp32, 64 MiB total)."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    if cfg == "C4":
+        chans = 8 if n >= 8 else max(1, n)
+        xmls = {"ar": xmlgen.allreduce_ring(n, chans, "Simple", True, 0, 1 << 40, name="c4_ring")}
+        dt, S = M.BFLOAT16, 256 << 20
+    elif cfg == "C5":
+        xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, 4, "Simple", False, 0, 1 << 40, name="c5_rs"),
+                "ag": xmlgen.allgather_allpairs(n, 4, "Simple", False, 0, 1 << 40, name="c5_ag")}
+        dt, S = M.FLOAT32, 64 << 20
+    else:
+        raise ValueError(cfg)
+    paths = []
+    for k, x in xmls.items():
+        pth = os.path.join(tmp, "bench_%s_%s_%d.xml" % (cfg, k, os.getpid()))
+        open(pth, "w").write(x)
+        paths.append(pth)
+    os.environ["MSCCL_XML_FILES"] = ":".join(paths)
+    comms = init_comms(multi, world, rank, n)
+    ts = M.TYPE_SIZE[dt]
+    stream = torch.cuda.Stream(dev)
+    nloc = len(comms)
+    try:
+        if cfg == "C4":
+            cnt = S // ts
+            bufs = [torch.zeros(S // 2, dtype=torch.int16, device=dev) for _ in range(nloc)]
+
+            def step():
+                with M.group():
+                    for c, b in zip(comms, bufs):
+                        c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+            phases = {"allreduce": (step, S * 2 * (n - 1) / n)}
+        else:
+            rc = S // ts // n
+            ins = [torch.empty(S // 4, dtype=torch.float32, device=dev).uniform_(-1, 1) for _ in range(nloc)]
+            mids = [torch.empty(rc, dtype=torch.float32, device=dev) for _ in range(nloc)]
+            outs = [torch.empty(S // 4, dtype=torch.float32, device=dev) for _ in range(nloc)]
+
+            def rs():
+                with M.group():
+                    for c, i, m in zip(comms, ins, mids):
+                        c.reduce_scatter(i.data_ptr(), m.data_ptr(), rc, dt, M.SUM, stream.cuda_stream)
+
+            def ag():
+                with M.group():
+                    for c, m, o in zip(comms, mids, outs):
+                        c.all_gather(m.data_ptr(), o.data_ptr(), rc, dt, stream.cuda_stream)
+            phases = {"reduce_scatter": (rs, S * (n - 1) / n), "all_gather": (ag, S * (n - 1) / n)}
+        res = {}
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for name, (fn, busbytes) in phases.items():
+            for _ in range(max(1, a.warmup)):
+                fn()
+            if multi:
+                torch.distributed.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            ev0.record(stream)
+            k = max(1, min(a.steps, 10))
+            for _ in range(k):
+                fn()
+            ev1.record(stream)
+            torch.cuda.synchronize()
+            if multi:
+                torch.distributed.barrier()
+            t = (time.perf_counter() - t0) / k
+            ev_ms = ev0.elapsed_time(ev1) / k
+            if multi:
+                tt = torch.tensor([t, ev_ms], dtype=torch.float64)
+                torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+                t, ev_ms = float(tt[0]), float(tt[1])
+            if any(c.async_error() != 0 for c in comms):
+                raise RuntimeError("kernel reported an error (timeout/abort)")
+            res[name] = {"ms": round(t * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+                         "busbw": round(busbytes / t / 1e9, 3), "steps": k}
+        res["bytes"] = S
+        res["dtype"] = {M.BFLOAT16: "bf16", M.FLOAT32: "f32"}[dt]
+        res["ranks"] = n
+        res["schedule"] = "allreduce_ring x%d Simple" % (8 if n >= 8 else max(1, n)) if cfg == "C4" else \
+            "reduce_scatter_allpairs + allgather_allpairs x4 Simple"
+        return res
+    finally:
+        for c in comms:
+            c.destroy()
+
+
 def main():
     a = parse()
     import torch
@@ -169,15 +271,12 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        obj = [M.get_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comms = [M.Comm.init_rank(world, obj[0], rank)]
         devs = [torch.device("cuda", local)]
         my_ranks = [rank]
     else:
-        comms = M.Comm.init_all([0] * n)
         devs = [torch.device("cuda", 0)] * n
         my_ranks = list(range(n))
+    comms = init_comms(multi, world, rank, n)
 
     def barrier():
         if multi:
@@ -268,6 +367,16 @@ def main():
     e2e = None
     if a.e2e and rank == 0 and not multi:
         e2e = measure_e2e(comms, n, maxb, dt, ts, stream, devs[0])
+    for c in comms:
+        c.destroy()
+    comms = []
+    extras = {}
+    which = a.extras if a.extras is not None else ("C4,C5" if multi and world == 8 else "")
+    for cfg in [w for w in which.split(",") if w]:
+        try:
+            extras[cfg] = run_extra(cfg, a, multi, world, rank, n, tmp)
+        except Exception as e:  # noqa: BLE001  (reported in the JSON line, the headline stands)
+            extras[cfg] = {"error": str(e)[:300]}
     cpu = None
     if not a.no_cpu and rank == 0:
         cpu = cpu_baseline(2 if not multi else n, maxb, dt if dt in (6, 7, 9) else 7, a.cpu_seconds)
@@ -289,6 +398,8 @@ def main():
     }
     if e2e:
         out["e2e"] = e2e
+    if extras:
+        out["configs"] = extras
     if rank == 0:
         print(json.dumps(out), flush=True)
     for c in comms:

@@ -36,6 +36,16 @@ int mscclAmdBootstrapAllgather(const ncclUniqueId* id, int rank, int nranks, con
 /* Number of thread blocks a launch of algorithm `algoIndex` uses on this rank. */
 int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex);
 
+/* Device event trace (NPKit-style, the reference's src/include/npkit/): enabled per communicator
+ * with MSCCL_AMD_TRACE=1 at init.  Each workgroup slot (tb * maxSplit + sub) records up to
+ * MSCCL_AMD_TRACE_EVENTS 16-byte events of its most recent launch:
+ *   struct { uint64_t ts;  // s_memrealtime, 100 MHz
+ *            uint16_t type; uint16_t step; uint32_t arg; }
+ * Event 0 of a slot is a header {ts = launch start, type = 0xFFFF, step = events, arg = epoch}.
+ * Copies the whole buffer (slots x events x 16 B) into out; *slots and *events receive the
+ * geometry.  Synchronises the device.  ncclInvalidUsage when tracing is off. */
+int mscclAmdTraceRead(ncclComm_t comm, void* out, size_t outBytes, int* slots, int* events);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,11 @@ from typing import List, Optional, Sequence
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmsccl_amd.so")
 
+# trace event layout (include/msccl_amd.h: mscclAmdTraceRead); types: 1 setup, 2 dep-wait done,
+# 3 primitive begin (arg = transfer type << 24 | elements), 4 primitive end, 5 end, 0xFFFF header
+TRACE_DTYPE = [("ts", "<u8"), ("type", "<u2"), ("step", "<u2"), ("arg", "<u4")]
+TRACE_TYPES = {1: "setup", 2: "dep", 3: "begin", 4: "end", 5: "done", 0xFFFF: "header"}
+
 # ncclDataType_t (nccl.h.in:125-140)
 INT8, UINT8, INT32, UINT32, INT64, UINT64, FLOAT16, FLOAT32, FLOAT64, BFLOAT16 = range(10)
 DTYPE_NAMES = {"int8": INT8, "uint8": UINT8, "int32": INT32, "uint32": UINT32, "int64": INT64,
@@ -81,6 +86,7 @@ def lib() -> ctypes.CDLL:
     L.mscclAmdCommInfo.argtypes = [vp, ctypes.c_char_p, sz]
     L.mscclAmdBootstrapAllgather.argtypes = [ctypes.POINTER(UniqueId), i, i, vp, sz, vp]
     L.mscclAmdAlgoBlocks.argtypes = [vp, i]
+    L.mscclAmdTraceRead.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
     _lib = L
     return L
 
@@ -207,6 +213,18 @@ class Comm:
 
     def algo_blocks(self, idx: int) -> int:
         return lib().mscclAmdAlgoBlocks(self.handle, idx)
+
+    def trace(self):
+        """Device event trace of the most recent launch (MSCCL_AMD_TRACE=1 at init):
+        numpy array [slot = tb * maxSplit + sub][event] of TRACE_DTYPE (include/msccl_amd.h)."""
+        import numpy as np
+        slots, events = ctypes.c_int(), ctypes.c_int()
+        _check(lib().mscclAmdTraceRead(self.handle, None, 0, ctypes.byref(slots), ctypes.byref(events)),
+               "mscclAmdTraceRead")
+        buf = np.zeros(slots.value * events.value, dtype=TRACE_DTYPE)
+        _check(lib().mscclAmdTraceRead(self.handle, buf.ctypes.data, buf.nbytes, ctypes.byref(slots),
+                                       ctypes.byref(events)), "mscclAmdTraceRead")
+        return buf.reshape(slots.value, events.value)
 
     # ---- collectives (pointers are device addresses, stream a hipStream_t or 0) ------------
     def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int = SUM, stream: int = 0) -> None:

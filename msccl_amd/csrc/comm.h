@@ -70,6 +70,8 @@ struct ncclComm {
 
   // MSCCL state
   uint64_t* dFlags = nullptr;
+  msccl::TraceEvent* dTrace = nullptr;   // MSCCL_AMD_TRACE: [216 * maxSplit][traceEvents]
+  int traceEvents = 0;
   void* scratch = nullptr;
   size_t scratchSize = 0;
   uint32_t workIndex = 1;    // host launch counter (the device epoch drives the flags)

@@ -4,6 +4,8 @@
 
 #include <sstream>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/msccl_amd.h"
 #include "algo.h"
 #include "bootstrap.h"
@@ -97,6 +99,21 @@ int mscclAmdBootstrapAllgather(const ncclUniqueId* id, int rank, int nranks, con
 int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex) {
   if (!commValid(comm) || algoIndex < 0 || algoIndex >= (int)comm->algos.size()) return -1;
   return comm->algos[algoIndex].nBlocks;
+}
+
+int mscclAmdTraceRead(ncclComm_t comm, void* out, size_t outBytes, int* slots, int* events) {
+  if (!commValid(comm)) return ncclInvalidArgument;
+  if (!comm->dTrace) return ncclInvalidUsage;
+  const int nSlots = kMaxTb * comm->maxSplit;
+  const size_t bytes = (size_t)nSlots * comm->traceEvents * sizeof(TraceEvent);
+  if (slots) *slots = nSlots;
+  if (events) *events = comm->traceEvents;
+  if (!out) return ncclSuccess;
+  if (outBytes < bytes) return ncclInvalidArgument;
+  if (hipSetDevice(comm->cudaDev) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(out, comm->dTrace, bytes, hipMemcpyDeviceToHost) != hipSuccess)
+    return ncclUnhandledCudaError;
+  return ncclSuccess;
 }
 
 }  // extern "C"

@@ -27,6 +27,21 @@ constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kM
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
 constexpr int kCounterWords = 16;      // uint64 words per launch counter (own 128-B line)
 
+// Device trace event (mscclAmdTraceRead).
+struct TraceEvent {
+  uint64_t ts;
+  uint16_t type, step;
+  uint32_t arg;
+};
+enum TraceType : uint16_t {
+  kEvSetup = 1,      // program staged, connections read
+  kEvDepWait = 2,    // dependency flags satisfied (step = transfer index)
+  kEvPrimBegin = 3,  // arg = transfer type << 24 | elements of this workgroup (capped)
+  kEvPrimEnd = 4,
+  kEvEnd = 5,        // workgroup done
+  kEvHeader = 0xFFFF
+};
+
 // LL FIFO line (ncclLLFifoLine, devcomm.h:35-48): two 8-B {4-B data, 4-B flag} granules.
 struct alignas(16) LLLine { uint32_t d0, f0, d1, f1; };
 
@@ -84,6 +99,10 @@ struct DevComm {
   // start; the last workgroup to finish (counted in *done) advances it for the next launch.
   uint64_t* epoch;
   uint32_t* done;
+  // NPKit-style trace (null = off): [slot = tb * maxSplit + sub][traceEvents]
+  struct TraceEvent* trace;
+  int32_t traceEvents;
+  int32_t pad2;
 };
 
 // One rank's share of a launch (the reference passes ncclDevComm* + a 64-B ncclWorkElem,

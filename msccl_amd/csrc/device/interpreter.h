@@ -6,8 +6,9 @@
 //   * per transfer: wait on dependency flags COMPUTE_FLAG(workIndex, iter, step) of other
 //     thread blocks of the same rank (123-140), split `count` by mscclMaxAllowedCount (146-150),
 //     dispatch to the primitive, publish the own flag when hasdep (198-201);
-//   * reductions: LL order d(+)s0(+)s1.. (prims_ll.h:347-362), Simple order (s0(+)s1..)(+)d
-//     (prims_simple.h:258-263), per-element d-first path when thisNelem < nthreads (157-170);
+//   * reductions: LL order acc=d, acc=fn(acc,s_i) (prims_ll.h:347-362), LL128 acc=fn(s_i,acc)
+//     (prims_ll128.h:381-392), Simple order (s0(+)s1..)(+)d (prims_simple.h:258-263),
+//     per-element d-first path o=fn(s_i,o) when thisNelem < nthreads (157-170);
 //   * recv-reduce: LL fn(peer, local) (prims_ll.h:282-287), Simple fn(local, peer).
 //
 // MI355X-native execution: wave64 workgroups of kNT threads, 16-B packs per lane, buffer
@@ -79,6 +80,19 @@ struct Interp {
   uint64_t t0;
   int tid;
   int refNthreads;
+  TraceEvent* trace;  // this workgroup's trace slot (null = tracing off)
+  int nev, maxEv;
+
+  __device__ __forceinline__ void ev(uint16_t type, uint16_t step, uint32_t arg) {
+    if (trace != nullptr && tid == 0 && nev < maxEv) {
+      TraceEvent e;
+      e.ts = __builtin_amdgcn_s_memrealtime();
+      e.type = type;
+      e.step = step;
+      e.arg = arg;
+      trace[nev++] = e;
+    }
+  }
 
   // ---------------------------------------------------------------- spins / abort
   __device__ __forceinline__ bool spinAbort(uint32_t& spins) {
@@ -140,36 +154,96 @@ struct Interp {
   }
   static __device__ __forceinline__ bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-  // ---------------------------------------------------------------- LL protocol
+  // ---------------------------------------------------------------- LL / LL128 protocols
+  // One primitive call is cut into FIFO steps of at most one slot (slotPacks packs); sender and
+  // receiver own the same packs, so they agree on the number of steps.  Two line formats share
+  // the LL FIFO memory:
+  //   LL    (prims_ll.h):  a 16-B line = two 8-B {4-B data, 4-B flag} granules; pack p of a step
+  //                        occupies lines llLineIdx(p, 0/1).
+  //   LL128 (CDNA4 form):  a 16-B line = {12 B data, 4-B flag}; 3 packs (12 dwords) travel as a
+  //                        unit of 4 lines.  The reference's LL128 (prims_ll128.h) relies on NVLink
+  //                        delivering a warp's 128-B line whole; CDNA4 documents no such
+  //                        guarantee, and a 16-B aligned store is the unit observed untorn on
+  //                        gfx950.  So the flag guards 12 B instead of 120 B: payload 75 % of the
+  //                        wire bytes instead of LL's 50 %.
+  // The values are the protocol's: recv-reduce fn(peer, local) for both.
+  static constexpr bool kL16 = PROTO == pLL128;
+
+  // LL128 line of (unit u, line j): 64 units keep line j of each in one contiguous 1 KiB
+  static __device__ __forceinline__ int l16LineIdx(int u, int j) { return ((u >> 6) << 8) + (j << 6) + (u & 63); }
+  static __device__ __forceinline__ int l16Lines(int nv) { return nv == 3 ? 4 : nv + 1; }  // lines for nv packs
+
   template <int RECV, int SEND, int SRC, int DST>
   __device__ void llOp(const T* src, T* dst, const Shape s) {
-    constexpr int E = 8 / TS;  // elements per line
+    constexpr int E = 8 / TS;  // elements per LL line
     const int nlinesFull = (s.n + E - 1) / E;
-    if (SEND) waitSendCredit();
-    LLLine* rslot = nullptr;
+    const int slotLines = SEND ? sc->llSlotLines : rc->llSlotLines;
+    const int slotPacks = kL16 ? (slotLines / 256) * 64 * 3 : slotLines / 2;
     __amdgpu_buffer_rsrc_t srs, drs, frs;
-    uint32_t rflag = 0, sflag = 0;
-    if (RECV) {
-      rslot = rc->ll + (recvStep % kFifoSteps) * (uint64_t)rc->llSlotLines;
-      rflag = (uint32_t)(recvStep + 1);
-    }
-    if (SEND) {
-      frs = makeRsrc(sc->ll + (sendStep % kFifoSteps) * (uint64_t)sc->llSlotLines);
-      sflag = (uint32_t)(sendStep + 1);
-    }
     if (SRC) srs = makeRsrc(src);
     if (DST) drs = makeRsrc(dst);
     const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
-    // U packs per lane per pass: all their loads and line polls in flight together
-    for (int base = tid; base < s.npk; base += kNT * U) {
+    int s0 = 0;
+    do {
+      const int s1 = s.npk - s0 < slotPacks ? s.npk : s0 + slotPacks;
+      if (SEND) waitSendCredit();
+      LLLine* rslot = nullptr;
+      uint32_t rflag = 0, sflag = 0;
+      if (RECV) {
+        rslot = rc->ll + (recvStep % kFifoSteps) * (uint64_t)rc->llSlotLines;
+        rflag = (uint32_t)(recvStep + 1);
+      }
+      if (SEND) {
+        frs = makeRsrc(sc->ll + (sendStep % kFifoSteps) * (uint64_t)sc->llSlotLines);
+        sflag = (uint32_t)(sendStep + 1);
+      }
+      if constexpr (kL16) {
+        l16Step<RECV, SEND, SRC, DST>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1);
+      } else {
+        llStep<RECV, SEND, SRC, DST>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1, nlinesFull);
+      }
+      if (SEND) {
+        if ((sendStep & kLLCleanMask) == kLLCleanMask) {
+          // LL cleanup (prims_ll.h:90-97): stamp every unused line of the slot with this flag
+          const int units = (s1 - s0 + 2) / 3;
+          for (int l = tid; l < slotLines; l += kNT) {
+            bool used;
+            if constexpr (kL16) {
+              const int u = ((l >> 8) << 6) + (l & 63), j = (l >> 6) & 3;
+              used = u < units && j < l16Lines(min(3, s1 - s0 - 3 * u));
+            } else {
+              const int q = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
+              used = s0 + q < s1 && 2 * s.bufPack(s0 + q) + h < nlinesFull;
+            }
+            if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
+          }
+        }
+        sendStep++;
+      }
+      if (RECV) {
+        recvStep++;
+        __syncthreads();
+        if (tid == 0) atomicStoreSys(rc->remoteHead, recvStep);
+      }
+      s0 = s1;
+    } while (s0 < s.npk);
+  }
+
+  // one LL step: packs [s0, s1) of the call, U packs per lane per pass with all their loads and
+  // line polls in flight together
+  template <int RECV, int SEND, int SRC, int DST>
+  __device__ void llStep(__amdgpu_buffer_rsrc_t srs, __amdgpu_buffer_rsrc_t drs,
+                                         __amdgpu_buffer_rsrc_t frs, LLLine* rslot, uint32_t rflag,
+                                         uint32_t sflag, bool vec, const Shape& s, int s0, int s1, int nlinesFull) {
+    for (int base = tid; base < s1 - s0; base += kNT * U) {
       int B[U];
       bool act[U], two[U];
       u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const int p = base + u * kNT;
-        act[u] = p < s.npk;
-        B[u] = act[u] ? s.bufPack(p) : 0;
+        const int q = base + u * kNT;
+        act[u] = q < s1 - s0;
+        B[u] = act[u] ? s.bufPack(s0 + q) : 0;
         two[u] = act[u] && 2 * B[u] + 1 < nlinesFull;
         v[u] = (u32x4){0, 0, 0, 0};
       }
@@ -183,9 +257,9 @@ struct Interp {
         u32x4 ln[2 * U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
-          const int p = base + u * kNT;
-          la[2 * u] = act[u] ? rslot + llLineIdx(p, 0) : rslot;
-          la[2 * u + 1] = two[u] ? rslot + llLineIdx(p, 1) : la[2 * u];
+          const int q = base + u * kNT;
+          la[2 * u] = act[u] ? rslot + llLineIdx(q, 0) : rslot;
+          la[2 * u + 1] = two[u] ? rslot + llLineIdx(q, 1) : la[2 * u];
         }
         ldLines8(la, ln);
 #pragma unroll
@@ -204,9 +278,9 @@ struct Interp {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           if (!act[u]) continue;
-          const int p = base + u * kNT;
-          st16<kAuxFifo>(frs, (uint32_t)llLineIdx(p, 0) * 16, (u32x4){v[u].x, sflag, v[u].y, sflag});
-          if (two[u]) st16<kAuxFifo>(frs, (uint32_t)llLineIdx(p, 1) * 16, (u32x4){v[u].z, sflag, v[u].w, sflag});
+          const int q = base + u * kNT;
+          st16<kAuxFifo>(frs, (uint32_t)llLineIdx(q, 0) * 16, (u32x4){v[u].x, sflag, v[u].y, sflag});
+          if (two[u]) st16<kAuxFifo>(frs, (uint32_t)llLineIdx(q, 1) * 16, (u32x4){v[u].z, sflag, v[u].w, sflag});
         }
       }
       if (DST) {
@@ -215,21 +289,88 @@ struct Interp {
           if (act[u]) storePack(drs, vec, B[u], s.n, v[u]);
       }
     }
-    if (SEND) {
-      if ((sendStep & kLLCleanMask) == kLLCleanMask) {
-        // LL cleanup (prims_ll.h:90-97): stamp every unused line of the slot with this flag
-        for (int l = tid; l < sc->llSlotLines; l += kNT) {
-          int p = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
-          bool used = p < s.npk && 2 * s.bufPack(p) + h < nlinesFull;
-          if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
+  }
+
+  // one LL128 step: units of 3 packs / 4 lines, two units per lane per pass (8 lines in flight)
+  template <int RECV, int SEND, int SRC, int DST>
+  __device__ void l16Step(__amdgpu_buffer_rsrc_t srs, __amdgpu_buffer_rsrc_t drs,
+                                          __amdgpu_buffer_rsrc_t frs, LLLine* rslot, uint32_t rflag,
+                                          uint32_t sflag, bool vec, const Shape& s, int s0, int s1) {
+    constexpr int UU = 2;
+    const int units = (s1 - s0 + 2) / 3;
+    for (int base = tid; base < units; base += kNT * UU) {
+      int nv[UU], B[UU][3];
+      u32x4 v[UU][3];
+#pragma unroll
+      for (int k = 0; k < UU; k++) {
+        const int u = base + k * kNT;
+        const int rem = u < units ? s1 - s0 - 3 * u : 0;
+        nv[k] = rem < 3 ? rem : 3;
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+          B[k][j] = j < nv[k] ? s.bufPack(s0 + 3 * u + j) : 0;
+          v[k][j] = (u32x4){0, 0, 0, 0};
         }
       }
-      sendStep++;
-    }
-    if (RECV) {
-      recvStep++;
-      __syncthreads();
-      if (tid == 0) atomicStoreSys(rc->remoteHead, recvStep);
+      if (SRC) {
+#pragma unroll
+        for (int k = 0; k < UU; k++)
+#pragma unroll
+          for (int j = 0; j < 3; j++)
+            if (j < nv[k]) v[k][j] = loadPack(srs, vec, B[k][j], s.n);
+      }
+      if (RECV) {
+        const void* la[4 * UU];
+        u32x4 ln[4 * UU];
+#pragma unroll
+        for (int k = 0; k < UU; k++) {
+          const int u = base + k * kNT;
+          const int nl = nv[k] > 0 ? l16Lines(nv[k]) : 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            la[4 * k + j] = j < nl ? (const void*)(rslot + l16LineIdx(u, j)) : (const void*)rslot;
+        }
+        ldLines8(la, ln);
+#pragma unroll
+        for (int k = 0; k < UU; k++) {
+          const int nl = nv[k] > 0 ? l16Lines(nv[k]) : 0;
+          uint32_t spins = 0;
+          while ((nl > 0 && ln[4 * k].w != rflag) || (nl > 1 && ln[4 * k + 1].w != rflag) ||
+                 (nl > 2 && ln[4 * k + 2].w != rflag) || (nl > 3 && ln[4 * k + 3].w != rflag)) {
+            if (spinAbort(spins)) break;
+            ldLines2(la[4 * k], la[4 * k + 1], ln[4 * k], ln[4 * k + 1]);
+            ldLines2(la[4 * k + 2], la[4 * k + 3], ln[4 * k + 2], ln[4 * k + 3]);
+          }
+          // 12 payload dwords of the unit -> 3 packs
+          const u32x4 p0 = {ln[4 * k].x, ln[4 * k].y, ln[4 * k].z, ln[4 * k + 1].x};
+          const u32x4 p1 = {ln[4 * k + 1].y, ln[4 * k + 1].z, ln[4 * k + 2].x, ln[4 * k + 2].y};
+          const u32x4 p2 = {ln[4 * k + 2].z, ln[4 * k + 3].x, ln[4 * k + 3].y, ln[4 * k + 3].z};
+          v[k][0] = SRC ? F::pack(p0, v[k][0]) : p0;
+          v[k][1] = SRC ? F::pack(p1, v[k][1]) : p1;
+          v[k][2] = SRC ? F::pack(p2, v[k][2]) : p2;
+        }
+      }
+      if (SEND) {
+#pragma unroll
+        for (int k = 0; k < UU; k++) {
+          if (nv[k] == 0) continue;
+          const int u = base + k * kNT;
+          const int nl = l16Lines(nv[k]);
+          st16<kAuxFifo>(frs, (uint32_t)l16LineIdx(u, 0) * 16, (u32x4){v[k][0].x, v[k][0].y, v[k][0].z, sflag});
+          st16<kAuxFifo>(frs, (uint32_t)l16LineIdx(u, 1) * 16, (u32x4){v[k][0].w, v[k][1].x, v[k][1].y, sflag});
+          if (nl > 2)
+            st16<kAuxFifo>(frs, (uint32_t)l16LineIdx(u, 2) * 16, (u32x4){v[k][1].z, v[k][1].w, v[k][2].x, sflag});
+          if (nl > 3)
+            st16<kAuxFifo>(frs, (uint32_t)l16LineIdx(u, 3) * 16, (u32x4){v[k][2].y, v[k][2].z, v[k][2].w, sflag});
+        }
+      }
+      if (DST) {
+#pragma unroll
+        for (int k = 0; k < UU; k++)
+#pragma unroll
+          for (int j = 0; j < 3; j++)
+            if (j < nv[k]) storePack(drs, vec, B[k][j], s.n, v[k][j]);
+      }
     }
   }
 
@@ -307,7 +448,7 @@ struct Interp {
   template <int RECV, int SEND, int SRC, int DST>
   __device__ __forceinline__ void op(const T* src, T* dst, const Shape s) {
     if constexpr (PROTO == pSimple) simpleOp<RECV, SEND, SRC, DST>(src, dst, s);
-    else llOp<RECV, SEND, SRC, DST>(src, dst, s);
+    else llOp<RECV, SEND, SRC, DST>(src, dst, s);  // LL and LL128
   }
 
   // ---------------------------------------------------------------- local ops
@@ -364,7 +505,8 @@ struct Interp {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           if constexpr (PROTO == pSimple) acc[u] = r == 0 ? x[u] : F::pack(acc[u], x[u]);  // (s0(+)s1..)(+)d
-          else acc[u] = F::pack(r == 0 ? d[u] : acc[u], x[u]);                             // d(+)s0(+)s1..
+          else if constexpr (PROTO == pLL128) acc[u] = F::pack(x[u], r == 0 ? d[u] : acc[u]);  // fn(s, acc)
+          else acc[u] = F::pack(r == 0 ? d[u] : acc[u], x[u]);                             // fn(acc, s)
         }
       }
 #pragma unroll
@@ -405,6 +547,10 @@ struct Interp {
     __syncthreads();
     sendStep = sh->step[0];
     recvStep = sh->step[1];
+    trace = comm->trace ? comm->trace + (size_t)(bid * maxSplit + sub) * comm->traceEvents : nullptr;
+    nev = 1;
+    maxEv = comm->traceEvents;
+    ev(kEvSetup, 0, 0);
 
     T* thisInput = (T*)w.sendbuff;
     T* thisOutput = (T*)w.recvbuff;
@@ -456,6 +602,7 @@ struct Interp {
           }
           step += t.numDeps - 1;
           __syncthreads();
+          ev(kEvDepWait, (uint16_t)i, 0);
         }
         T* srcP = t.srcbuf == 0 ? thisInput : (t.srcbuf == 1 ? thisOutput : thisScratch);
         T* dstP = t.dstbuf == 0 ? thisInput : (t.dstbuf == 1 ? thisOutput : thisScratch);
@@ -476,6 +623,7 @@ struct Interp {
             s.Lq = q1 - q0;
             s.npk = thisCount * s.Lq;
           }
+          ev(kEvPrimBegin, (uint16_t)i, ((uint32_t)t.type << 24) | (uint32_t)min(s.npk * PE, 0xFFFFFF));
           switch (t.type) {
             case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
             case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, s); break;
@@ -493,6 +641,7 @@ struct Interp {
             default: stop = true; break;  // MSCCL_RES_ADD / unknown: the tb ends (interpreter.h:195-196)
           }
           if (stop) break;
+          ev(kEvPrimEnd, (uint16_t)i, 0);
         }
         if (stop) break;
         if (t.hasDep) {
@@ -509,10 +658,19 @@ struct Interp {
       if (sc) sc->step = sendStep;
       if (rc) rc->step = recvStep;
       // the last workgroup of this rank's launch advances the epoch for the next launch
-      if (__hip_atomic_fetch_add(comm->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)w.nBlocks - 1) {
+      if (__hip_atomic_fetch_add(comm->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)w.nBlocks - 1) {
         __hip_atomic_store(comm->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         atomicStoreAgent(comm->epoch, workIndex + 1);
       }
+    }
+    ev(kEvEnd, 0, 0);
+    if (trace != nullptr && tid == 0) {
+      TraceEvent h;
+      h.ts = t0;
+      h.type = kEvHeader;
+      h.step = (uint16_t)nev;
+      h.arg = (uint32_t)workIndex;
+      trace[0] = h;
     }
   }
 };

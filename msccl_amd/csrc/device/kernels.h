@@ -1,5 +1,5 @@
 // Kernel instantiation + host launch shim (one translation unit per element type so the
-// 80 kernels build in parallel).
+// 120 kernels build in parallel).
 #pragma once
 #include "interpreter.h"
 
@@ -11,11 +11,11 @@ int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-#define MSCCL_DEFINE_TABLE(NAME, T)                                                      \
-  LaunchFn NAME[4][3] = {                                                                \
-      {launchKernel<T, kSum, pLL>, nullptr, launchKernel<T, kSum, pSimple>},             \
-      {launchKernel<T, kProd, pLL>, nullptr, launchKernel<T, kProd, pSimple>},           \
-      {launchKernel<T, kMax, pLL>, nullptr, launchKernel<T, kMax, pSimple>},             \
-      {launchKernel<T, kMin, pLL>, nullptr, launchKernel<T, kMin, pSimple>}};
+#define MSCCL_DEFINE_TABLE(NAME, T)                                                                 \
+  LaunchFn NAME[4][3] = {                                                                           \
+      {launchKernel<T, kSum, pLL>, launchKernel<T, kSum, pLL128>, launchKernel<T, kSum, pSimple>},             \
+      {launchKernel<T, kProd, pLL>, launchKernel<T, kProd, pLL128>, launchKernel<T, kProd, pSimple>},           \
+      {launchKernel<T, kMax, pLL>, launchKernel<T, kMax, pLL128>, launchKernel<T, kMax, pSimple>},             \
+      {launchKernel<T, kMin, pLL>, launchKernel<T, kMin, pLL128>, launchKernel<T, kMin, pSimple>}};
 
 }  // namespace msccl

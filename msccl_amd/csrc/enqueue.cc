@@ -83,7 +83,6 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   for (auto& r : comm->regs)
     if (r.algoIndex == idx) protoOverride = r.proto;
   NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, &out->plan));
-  if (out->plan.proto == kProtoLL128) out->plan.proto = kProtoLL;  // LL128 schedules run on the LL path
   if (out->plan.scratchNeeded > comm->scratchSize) {
     WARN("MSCCL: MSCCL scratch pad size is smaller than expected %zu < %zu", comm->scratchSize, out->plan.scratchNeeded);
     return ncclInternalError;
@@ -118,14 +117,14 @@ RankWork makeWork(Planned& p) {
   w.nBlocks = (int16_t)(da.nBlocks * split);
   // Consecutive full interpreter iterations can run as one: every element still sees the same
   // operations in the same order (only a partial last iteration can take the per-element reduce
-  // path, and it stays an iteration of its own).  An LL step of a sub-connection must still fit
-  // one FIFO slot, so at most `split` LL iterations merge.  maxAllowedCount is 1 whenever there
-  // is more than one iteration, so one op never exceeds M chunks.
+  // path, and it stays an iteration of its own).  Primitive calls are cut into FIFO-slot steps on
+  // the device, so any merge fits; LL merges `split` iterations (one slot per sub-connection
+  // step, as unmerged with one workgroup), Simple 4.  maxAllowedCount is 1 whenever there is
+  // more than one iteration, so one op never exceeds `merge` chunks.
   int merge = 1;
   if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {
     const int64_t envMerge = envInt("MSCCL_AMD_MERGE", 0);
     merge = envMerge > 0 ? (int)envMerge : (p.plan.proto == kProtoSimple ? 4 : split);
-    if (p.plan.proto != kProtoSimple) merge = std::min(merge, split);
     merge = std::max(1, std::min(merge, 64));
   }
   w.merge = (uint8_t)merge;

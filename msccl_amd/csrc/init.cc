@@ -134,6 +134,14 @@ ncclResult_t commFinish(ncclComm* comm) {
   dc.errWord = comm->devErr;
   dc.timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
   dc.maxSplit = comm->maxSplit;
+  if (envInt("MSCCL_AMD_TRACE", 0) > 0) {
+    comm->traceEvents = (int)std::max<int64_t>(8, std::min<int64_t>(65535, envInt("MSCCL_AMD_TRACE_EVENTS", 256)));
+    size_t bytes = (size_t)kMaxTb * comm->maxSplit * comm->traceEvents * sizeof(TraceEvent);
+    NCCLCHECK(hipErr(hipMalloc(&comm->dTrace, bytes), "hipMalloc trace"));
+    NCCLCHECK(hipErr(hipMemset(comm->dTrace, 0, bytes), "hipMemset trace"));
+    dc.trace = comm->dTrace;
+    dc.traceEvents = comm->traceEvents;
+  }
   dc.epoch = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
   dc.done = (uint32_t*)(dc.epoch + kCounterWords);
   NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
@@ -228,6 +236,7 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
   if (comm->dRecv) hipFree(comm->dRecv);
   if (comm->dComm) hipFree(comm->dComm);
   if (comm->dFlags) hipFree(comm->dFlags);
+  if (comm->dTrace) hipFree(comm->dTrace);
   if (comm->scratch) hipFree(comm->scratch);
   if (comm->boot && comm->ownsBoot) {
     if (peerBarrier) comm->boot->barrier();  // peers may still read our arena until everyone is done

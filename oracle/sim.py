@@ -8,7 +8,10 @@ semantics of the reference's device path:
                          COMPUTE_FLAG(workIndex, iter, step); `ra` and unknown types end the tb)
   LL primitives         device/prims_ll.h:247-380
                         recv-reduce: fn(peer, local)              (prims_ll.h:282-287)
-                        reduce:      ((d (+) s0) (+) s1) ...      (prims_ll.h:347-362)
+                        reduce:      acc = d; acc = fn(acc, s_i)  (prims_ll.h:347-362)
+  LL128 primitives      device/prims_ll128.h:184-425
+                        recv-reduce: fn(peer, local)              (prims_ll128.h:235-236)
+                        reduce:      acc = d; acc = fn(s_i, acc)  (prims_ll128.h:381-392)
   Simple primitives     device/prims_simple.h:131-281, common_kernel.h:490-690
                         recv-reduce: fn(local, peer)              (srcs = [local, peer], left fold)
                         reduce:      ((s0 (+) s1) ...) (+) d      (dst appended last, prims_simple.h:258-263)
@@ -104,10 +107,15 @@ def _tb_program(algo: L.Algorithm, bid: int, rank: int, plan: P.Plan, bufs, fifo
                         srcs.append(src[so:so + n].copy())
                     d = dst[dstoff:dstoff + n].copy()
                     if n < nthreads or proto != L.PROTO_SIMPLE:
-                        # LL / LL128 order, and the small path of every protocol: dst first
+                        # LL / LL128 order, and the small path of every protocol: dst first;
+                        # LL folds fn(acc, s) (prims_ll.h:352-358), LL128 and the small path
+                        # fn(s, acc) (prims_ll128.h:381-392, msccl_interpreter.h:163-166)
                         acc = d
                         for s in srcs:
-                            acc = N.apply(op, dt, s, acc) if n < nthreads else N.apply(op, dt, acc, s)
+                            if n < nthreads or proto == L.PROTO_LL128:
+                                acc = N.apply(op, dt, s, acc)
+                            else:
+                                acc = N.apply(op, dt, acc, s)
                     else:
                         acc = srcs[0]
                         for s in srcs[1:]:

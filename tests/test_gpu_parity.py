@@ -29,7 +29,7 @@ def check(xml, n, coll, count, dt, op=0, inplace=True, seed=1, mode="uniform", i
 
 
 # all-pairs AllReduce: protocol x dtype x size (small reduce path, multi-iteration, maxAllowedCount split)
-@pytest.mark.parametrize("proto", ["LL", "Simple"])
+@pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
 @pytest.mark.parametrize("dt", [7, 6, 9])
 @pytest.mark.parametrize("n,inst,count", [
     (2, 1, 4 * 8),            # 128 B fp32: smallest C2 point, per-element reduce path
@@ -43,12 +43,12 @@ def test_allpairs_allreduce(proto, dt, n, inst, count):
     check(xmlgen.allreduce_allpairs(n, inst, proto), n, L.ALLREDUCE, count, dt)
 
 
-@pytest.mark.parametrize("proto", ["LL", "Simple"])
+@pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
 def test_allpairs_out_of_place(proto):
     check(xmlgen.allreduce_allpairs(8, 2, proto, inplace=False), 8, L.ALLREDUCE, 128 * 513, 7, inplace=False)
 
 
-@pytest.mark.parametrize("proto,dt", [("Simple", 9), ("LL", 7), ("Simple", 6)])
+@pytest.mark.parametrize("proto,dt", [("Simple", 9), ("LL", 7), ("Simple", 6), ("LL128", 9), ("LL128", 8)])
 def test_ring_allreduce(proto, dt):
     check(xmlgen.allreduce_ring(8, 4, proto), 8, L.ALLREDUCE, 32 * 20000, dt)
 
@@ -70,13 +70,13 @@ def test_integer_types(dt):
     check(xmlgen.allreduce_allpairs(2, 2, "LL"), 2, L.ALLREDUCE, 8 * 999, dt, op=2)
 
 
-@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("Simple", True)])
+@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("Simple", True), ("LL128", False)])
 def test_reduce_scatter(proto, inplace):
     check(xmlgen.reduce_scatter_allpairs(8, 2, proto, inplace=inplace), 8, L.REDUCE_SCATTER, 2 * 50000, 7,
           inplace=inplace)
 
 
-@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("LL", False)])
+@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("LL", False), ("LL128", True)])
 def test_all_gather(proto, inplace):
     check(xmlgen.allgather_allpairs(8, 2, proto, inplace=inplace), 8, L.ALLGATHER, 2 * 33333, 7, inplace=inplace)
 
@@ -129,7 +129,7 @@ def test_golden_vectors_on_gpu(name):
 
 
 @pytest.mark.parametrize("split", [1, 2, 8])
-@pytest.mark.parametrize("proto", ["LL", "Simple"])
+@pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
 def test_workgroup_split_is_value_neutral(split, proto, monkeypatch):
     """Running each XML thread block as `split` workgroups (sub-connections) changes no bit."""
     monkeypatch.setenv("MSCCL_AMD_SPLIT", str(split))
@@ -142,6 +142,8 @@ def test_workgroup_split_is_value_neutral(split, proto, monkeypatch):
     ("LL", 8192 * 3 + 100, 7),        # 3 full LL iterations (merged) + a partial one on the per-element path
     ("LL", 8192 * 5, 9),              # bf16: 2.5 LL iterations
     ("Simple", 524288 * 2 + 1000, 7),  # 2 full Simple iterations (merged) + a partial one
+    ("LL128", 144000 * 2 + 60, 7),     # 2 full LL128 iterations (576000-B steps) + a partial one
+    ("LL", 8192 * 16, 7),              # 16 iterations: merged steps longer than one FIFO slot
 ])
 def test_merged_iterations_are_value_neutral(proto, per_chunk, dt):
     """Consecutive full interpreter iterations run as one op (RankWork.merge): bit-exact vs the
@@ -149,3 +151,40 @@ def test_merged_iterations_are_value_neutral(proto, per_chunk, dt):
     x = xmlgen.allreduce_allpairs(2, 1, proto)
     ncpl = 4
     check(x, 2, L.ALLREDUCE, ncpl * per_chunk, dt)
+
+
+@pytest.mark.parametrize("op", [0, 2])
+@pytest.mark.parametrize("dt", [6, 8, 0])
+def test_ll128_types_and_ops(op, dt):
+    """LL128 (CDNA4 16-B line form): 3 packs per 4 lines, partial units, every element width."""
+    for count in (16 * 3 * 7 + 5 * 16, 64 * 1001):
+        check(xmlgen.allreduce_allpairs(4, 2, "LL128"), 4, L.ALLREDUCE, count, dt, op=op,
+              mode="exact" if dt == 0 else "uniform")
+
+
+def test_ll_and_ll128_share_a_fifo(tmp_path):
+    """An LL and an LL128 schedule on the same connections, alternating launches on the same
+    communicators: the flag words of either line format never satisfy the other's wait."""
+    import torch
+    import msccl_amd as M
+    a = tmp_path / "ll.xml"
+    b = tmp_path / "ll128.xml"
+    a.write_text(xmlgen.allreduce_allpairs(2, 1, "LL", min_bytes=0, max_bytes=1 << 16))
+    b.write_text(xmlgen.allreduce_allpairs(2, 1, "LL128", min_bytes=1 << 16, max_bytes=1 << 30))
+    os.environ["MSCCL_XML_FILES"] = "%s:%s" % (a, b)
+    comms = M.Comm.init_all([0, 0])
+    try:
+        g = torch.Generator().manual_seed(5)
+        for it, count in enumerate([4 * 1000, 4 * 40000] * 4):
+            x = [torch.randint(-4, 5, (count,), generator=g).float() for _ in range(2)]
+            d = [t.cuda() for t in x]
+            with M.group():
+                for c, t in zip(comms, d):
+                    c.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, 0)
+            torch.cuda.synchronize()
+            for t in d:
+                assert torch.equal(t.cpu(), x[0] + x[1]), it
+        assert all(c.async_error() == 0 for c in comms)
+    finally:
+        for c in comms:
+            c.destroy()

@@ -230,3 +230,42 @@ def test_hip_graph_capture_and_replay(proto, tmp_path):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_device_trace_records_every_transfer(tmp_path, monkeypatch):
+    """MSCCL_AMD_TRACE=1: every workgroup of the last launch leaves a header, a setup event, a
+    begin/end pair per executed transfer and an end event, in time order."""
+    import torch
+    import msccl_amd as M
+    from msccl_amd import xmlgen
+    xml = tmp_path / "ap.xml"
+    xml.write_text(xmlgen.allreduce_allpairs(2, 1, "LL"))
+    monkeypatch.setenv("MSCCL_XML_FILES", str(xml))
+    monkeypatch.setenv("MSCCL_AMD_TRACE", "1")
+    comms = M.Comm.init_all([0, 0])
+    try:
+        bufs = [torch.ones(4 * 256, device="cuda") for _ in comms]
+        for _ in range(3):
+            with M.group():
+                for c, b in zip(comms, bufs):
+                    c.all_reduce(b.data_ptr(), b.data_ptr(), 4 * 256, M.FLOAT32, M.SUM, 0)
+        torch.cuda.synchronize()
+        algo = M.algo_json(str(xml), 0, 2)
+        for c in comms:
+            tr = c.trace()
+            info = c.info()
+            split = info["maxSplit"]
+            used = [s for s in range(tr.shape[0]) if tr[s, 0]["type"] == 0xFFFF]
+            assert len(used) >= len(algo["tbs"])
+            for s in used:
+                n = int(tr[s, 0]["step"])
+                ev = tr[s, 1:n]
+                assert ev[0]["type"] == 1 and ev[-1]["type"] == 5
+                assert np.all(np.diff(ev["ts"].astype(np.int64)) >= 0)
+                tb = algo["tbs"][s // split]
+                assert int((ev["type"] == 3).sum()) == len(tb["transfers"])
+                assert int((ev["type"] == 4).sum()) == len(tb["transfers"])
+            assert int(tr[used[0], 0]["arg"]) == 3  # epoch of the third launch
+    finally:
+        for c in comms:
+            c.destroy()
