@@ -25,7 +25,6 @@ constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag
 constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
 constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kMaxSplit
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
-constexpr int kCounterWords = 16;      // uint64 words per launch counter (own 128-B line)
 
 // Device trace event (mscclAmdTraceRead).
 struct TraceEvent {
@@ -69,6 +68,7 @@ struct DevSendConn {
   uint64_t* remoteTail;         // receiver's tail word (peer memory)
   uint64_t* head;               // my head word, written by the receiver
   uint64_t step;                // persistent step counter (owned by one workgroup)
+  uint64_t headSeen;            // last head value read: credit known without a poll while step < headSeen + 8
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
   int32_t remote;               // receiver on another GPU: system-scope release before a tail post
@@ -81,6 +81,7 @@ struct DevRecvConn {
   uint64_t* tail;               // my tail word, written by the sender
   uint64_t* remoteHead;         // sender's head word (peer memory)
   uint64_t step;
+  uint64_t tailSeen;            // last Simple tail value read (data known present below it)
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
 };
@@ -95,10 +96,14 @@ struct DevComm {
   int32_t maxSplit;             // sub-connections per (channel, peer): conn k of key c = send[c*maxSplit+k]
   int32_t pad;
   // Launch epoch (the reference's host-side workIndex, enqueue.cc:714-721, kept on the device so
-  // that a captured hipGraph replays correctly): every workgroup of a launch reads *epoch at
-  // start; the last workgroup to finish (counted in *done) advances it for the next launch.
-  uint64_t* epoch;
-  uint32_t* done;
+  // that a captured hipGraph replays correctly), one word per workgroup slot
+  // (slot = tb * maxSplit + sub, the flag index): a workgroup reads its own slot at start and
+  // writes slot + 1 at its end, together with the slots this launch does not run (tbs beyond
+  // the schedule's, subs beyond its split).  Every slot therefore holds the same value at every
+  // launch start, and no counter is shared by the workgroups of a launch (a contended
+  // "last one out" counter cost several us per launch at 512 workgroups).
+  uint64_t* epochs;             // [kFlagSlots]
+  uint64_t* unused;
   // NPKit-style trace (null = off): [slot = tb * maxSplit + sub][traceEvents]
   struct TraceEvent* trace;
   int32_t traceEvents;

@@ -37,7 +37,10 @@ struct alignas(16) BlockShared {
   int16_t depBid[256];
   int16_t depStep[256];
   int16_t red[256];
+  DevSendConn sconn;  // this workgroup's connections, copied once per launch (no global
+  DevRecvConn rconn;  // load of connection metadata on the primitives' critical path)
   uint64_t step[2];
+  uint64_t seen[2];  // send head / recv tail last observed
   uint64_t epoch;
   uint32_t aborted;
 };
@@ -74,9 +77,12 @@ struct Interp {
 
   BlockShared* sh;
   DevComm* comm;
-  DevSendConn* sc;
+  DevSendConn* sc;   // LDS copies (read-only in the primitives)
   DevRecvConn* rc;
+  DevSendConn* scG;  // global connection state (step counters written back at the end)
+  DevRecvConn* rcG;
   uint64_t sendStep, recvStep;
+  uint64_t headSeen, tailSeen;  // credit / Simple data known available without polling
   uint64_t t0;
   int tid;
   int refNthreads;
@@ -110,14 +116,35 @@ struct Interp {
     return false;
   }
 
+  // Send credit: the receiver has freed slot `sendStep` once head + kFifoSteps > sendStep.  The
+  // last head seen is kept (and persisted in the connection), so most steps need no poll of the
+  // remote word, whose round trip is the largest part of a small message's latency.
   __device__ __forceinline__ void waitSendCredit() {
+    if (headSeen + kFifoSteps >= sendStep + 1) return;
     if (tid == 0) {
       uint32_t spins = 0;
-      while (atomicLoadSys(sc->head) + kFifoSteps < sendStep + 1) {
+      uint64_t h;
+      while ((h = atomicLoadSys(sc->head)) + kFifoSteps < sendStep + 1) {
         if (spinAbort(spins)) break;
       }
+      sh->seen[0] = h;
     }
     __syncthreads();
+    headSeen = uni(sh->seen[0]);
+  }
+  // Simple data: the sender has posted step recvStep once tail > recvStep
+  __device__ __forceinline__ void waitRecvTail() {
+    if (tailSeen >= recvStep + 1) return;
+    if (tid == 0) {
+      uint32_t spins = 0;
+      uint64_t t;
+      while ((t = atomicLoadSys(rc->tail)) < recvStep + 1) {
+        if (spinAbort(spins)) break;
+      }
+      sh->seen[1] = t;
+    }
+    __syncthreads();
+    tailSeen = uni(sh->seen[1]);
   }
 
   // ---------------------------------------------------------------- pack helpers
@@ -177,7 +204,7 @@ struct Interp {
   __device__ void llOp(const T* src, T* dst, const Shape s) {
     constexpr int E = 8 / TS;  // elements per LL line
     const int nlinesFull = (s.n + E - 1) / E;
-    const int slotLines = SEND ? sc->llSlotLines : rc->llSlotLines;
+    const int slotLines = uni(SEND ? sc->llSlotLines : rc->llSlotLines);
     const int slotPacks = kL16 ? (slotLines / 256) * 64 * 3 : slotLines / 2;
     __amdgpu_buffer_rsrc_t srs, drs, frs;
     if (SRC) srs = makeRsrc(src);
@@ -377,7 +404,7 @@ struct Interp {
   // ---------------------------------------------------------------- Simple protocol
   template <int RECV, int SEND, int SRC, int DST>
   __device__ void simpleOp(const T* src, T* dst, const Shape s) {
-    const int slotBytes = SEND ? sc->simpleSlotBytes : rc->simpleSlotBytes;
+    const int slotBytes = uni(SEND ? sc->simpleSlotBytes : rc->simpleSlotBytes);
     const int slicePacks = slotBytes / 16;
     __amdgpu_buffer_rsrc_t srs, drs, rrs, frs;
     if (SRC) srs = makeRsrc(src);
@@ -385,15 +412,8 @@ struct Interp {
     const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
     for (int s0 = 0; s0 < s.npk; s0 += slicePacks) {
       const int s1 = s.npk - s0 < slicePacks ? s.npk : s0 + slicePacks;
-      if (tid == 0) {
-        uint32_t spins = 0;
-        if (RECV)
-          while (atomicLoadSys(rc->tail) < recvStep + 1)
-            if (spinAbort(spins)) break;
-        if (SEND)
-          while (atomicLoadSys(sc->head) + kFifoSteps < sendStep + 1)
-            if (spinAbort(spins)) break;
-      }
+      if (RECV) waitRecvTail();
+      if (SEND) waitSendCredit();
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
@@ -452,7 +472,7 @@ struct Interp {
   }
 
   // ---------------------------------------------------------------- local ops
-  __device__ void localCopy(const T* src, T* dst, const Shape s) {
+  __device__ __forceinline__ void localCopy(const T* src, T* dst, const Shape s) {
     __amdgpu_buffer_rsrc_t srs = makeRsrc(src), drs = makeRsrc(dst);
     const bool vec = aligned16(src) && aligned16(dst);
     for (int base = tid; base < s.npk; base += kNT * U) {
@@ -468,17 +488,24 @@ struct Interp {
 
   // Source r of the fused reduction starts at srcBase + chunkOff + reds[r] * sizePer (reds: chunk
   // indices in LDS, at most MSCCL_MAX_REDUCE_FUSION = 16).  The per-element path is chosen on the whole call's element count, as in the reference.
-  __device__ void reduce(const T* srcBase, const int16_t* reds, int64_t chunkOff, int64_t sizePer, int nsrc, T* dst,
+  __device__ __forceinline__ void reduce(const T* srcBase, const int16_t* reds, int64_t chunkOff, int64_t sizePer, int nsrc, T* dst,
                          const Shape s) {
     if (s.n < refNthreads) {
       // per-element path, d first: o = fn(s_r, o) (msccl_interpreter.h:157-170)
       __amdgpu_buffer_rsrc_t drs = makeRsrc(dst);
+      // all (at most MSCCL_MAX_REDUCE_FUSION) sources are loaded before the fold, so the
+      // element costs one memory round trip instead of one per source
       for (int k = tid; k < s.npk * PE; k += kNT) {
         const int e = s.bufPack(k / PE) * PE + (k % PE);
         if (e >= s.n) continue;
         T o = ldElem<T>(drs, (uint32_t)e * TS);
-        for (int r = 0; r < nsrc; r++)
-          o = F::elem(ldElem<T>(makeRsrc(srcBase + chunkOff + reds[r] * sizePer), (uint32_t)e * TS), o);
+        T x[16];
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+          if (r < nsrc) x[r] = ldElem<T>(makeRsrc(srcBase + chunkOff + reds[r] * sizePer), (uint32_t)e * TS);
+#pragma unroll
+        for (int r = 0; r < 16; r++)
+          if (r < nsrc) o = F::elem(x[r], o);
         stElem<T>(drs, (uint32_t)e * TS, o);
       }
       return;
@@ -519,14 +546,20 @@ struct Interp {
   }
 
   // ---------------------------------------------------------------- the interpreter loop
-  __device__ void run(const RankWork& w, int bid, int sub) {
+  __device__ __forceinline__ void run(const RankWork& w, int bid, int sub) {
     tid = threadIdx.x;
     comm = w.comm;
     refNthreads = w.refNthreads;
     t0 = __builtin_amdgcn_s_memrealtime();
     const int split = w.split;
     const int maxSplit = comm->maxSplit;
-    const DevTbHeader hd = w.tbs[bid];
+    const int slot = bid * maxSplit + sub;  // flag / epoch / trace slot of this workgroup
+    DevTbHeader hd;
+    {
+      u32x4 raw = *(const u32x4*)&w.tbs[bid];
+      raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
+      __builtin_memcpy(&hd, &raw, sizeof(hd));
+    }
     // stage the tb program in LDS
     const DevTransfer* gtr = (const DevTransfer*)(w.blob + hd.blobOffset);
     const int16_t* gdep = (const int16_t*)(gtr + hd.nsteps);
@@ -536,18 +569,28 @@ struct Interp {
       sh->depStep[i] = gdep[hd.ndeps + i];
     }
     for (int i = tid; i < hd.nreds; i += kNT) sh->red[i] = gdep[2 * hd.ndeps + i];
-    sc = hd.sendConn >= 0 ? comm->send + (size_t)hd.sendConn * maxSplit + sub : nullptr;
-    rc = hd.recvConn >= 0 ? comm->recv + (size_t)hd.recvConn * maxSplit + sub : nullptr;
+    scG = hd.sendConn >= 0 ? comm->send + (size_t)hd.sendConn * maxSplit + sub : nullptr;
+    rcG = hd.recvConn >= 0 ? comm->recv + (size_t)hd.recvConn * maxSplit + sub : nullptr;
+    static_assert(sizeof(DevSendConn) % 4 == 0 && sizeof(DevRecvConn) % 4 == 0, "connection copy");
+    constexpr int kSW = sizeof(DevSendConn) / 4, kRW = sizeof(DevRecvConn) / 4;
+    if (scG && tid < kSW) ((uint32_t*)&sh->sconn)[tid] = ((const uint32_t*)scG)[tid];
+    if (rcG && tid >= 64 && tid < 64 + kRW) ((uint32_t*)&sh->rconn)[tid - 64] = ((const uint32_t*)rcG)[tid - 64];
+    sc = scG ? &sh->sconn : nullptr;
+    rc = rcG ? &sh->rconn : nullptr;
     if (tid == 0) {
-      sh->step[0] = sc ? sc->step : 0;
-      sh->step[1] = rc ? rc->step : 0;
+      sh->step[0] = scG ? scG->step : 0;
+      sh->step[1] = rcG ? rcG->step : 0;
+      sh->seen[0] = scG ? scG->headSeen : 0;
+      sh->seen[1] = rcG ? rcG->tailSeen : 0;
       sh->aborted = 0;
-      sh->epoch = atomicLoadAgent(comm->epoch);
+      sh->epoch = atomicLoadAgent(comm->epochs + slot);
     }
     __syncthreads();
-    sendStep = sh->step[0];
-    recvStep = sh->step[1];
-    trace = comm->trace ? comm->trace + (size_t)(bid * maxSplit + sub) * comm->traceEvents : nullptr;
+    sendStep = uni(sh->step[0]);
+    recvStep = uni(sh->step[1]);
+    headSeen = uni(sh->seen[0]);
+    tailSeen = uni(sh->seen[1]);
+    trace = comm->trace ? comm->trace + (size_t)slot * comm->traceEvents : nullptr;
     nev = 1;
     maxEv = comm->traceEvents;
     ev(kEvSetup, 0, 0);
@@ -558,7 +601,7 @@ struct Interp {
     const int64_t sizePer = w.sizePerChunk;
     const int64_t chunkSize = w.chunkSize;
     const int mac = w.maxAllowedCount;
-    const uint64_t workIndex = sh->epoch;  // COMPUTE_FLAG's workIndex (msccl_interpreter.h:14-16)
+    const uint64_t workIndex = uni(sh->epoch);  // COMPUTE_FLAG's workIndex (msccl_interpreter.h:14-16)
     uint64_t* flags = comm->flags;
     bool stop = false;
 
@@ -587,7 +630,12 @@ struct Interp {
       const int q0 = (int)((int64_t)Qc * sub / split), q1 = (int)((int64_t)Qc * (sub + 1) / split);
       int step = 0;
       for (int i = 0; i < hd.nsteps; i++) {
-        const DevTransfer t = sh->tr[i];
+        DevTransfer t;
+        {
+          u32x4 raw = *(const u32x4*)&sh->tr[i];
+          raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
+          __builtin_memcpy(&t, &raw, sizeof(t));
+        }
         if (t.numDeps > 0) {
           // the same positions of the thread blocks this transfer depends on (interpreter.h:123-140)
           if (tid < t.numDeps) {
@@ -595,7 +643,7 @@ struct Interp {
             const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)sh->depStep[t.depPtr + tid]);
             uint32_t spins = 0;
             while (true) {
-              uint64_t cur = atomicLoadAgent(flags + ((size_t)db * split + sub) * kFlagStride);
+              uint64_t cur = atomicLoadAgent(flags + ((size_t)db * maxSplit + sub) * kFlagStride);
               if (cur >= goal && (cur >> 24) == workIndex) break;
               if (spinAbort(spins)) break;
             }
@@ -648,20 +696,29 @@ struct Interp {
           drainStores();
           __syncthreads();
           if (tid == 0)
-            atomicStoreAgent(flags + ((size_t)bid * split + sub) * kFlagStride, computeFlag(workIndex, iter, step));
+            atomicStoreAgent(flags + (size_t)slot * kFlagStride, computeFlag(workIndex, iter, step));
         }
         step++;
       }
     }
     __syncthreads();
     if (tid == 0) {
-      if (sc) sc->step = sendStep;
-      if (rc) rc->step = recvStep;
-      // the last workgroup of this rank's launch advances the epoch for the next launch
-      if (__hip_atomic_fetch_add(comm->done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)w.nBlocks - 1) {
-        __hip_atomic_store(comm->done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicStoreAgent(comm->epoch, workIndex + 1);
+      if (scG) {
+        scG->step = sendStep;
+        scG->headSeen = headSeen;
       }
+      if (rcG) {
+        rcG->step = recvStep;
+        rcG->tailSeen = tailSeen;
+      }
+      atomicStoreAgent(comm->epochs + slot, workIndex + 1);
+    }
+    {
+      // advance the epoch of every slot this launch does not run (DevComm::epochs): launch
+      // workgroup g covers the unlaunched slots j with j % launched == g
+      const int launched = w.nBlocks, nTb = launched / split, g = bid * split + sub;
+      for (int j = g + tid * launched; j < kFlagSlots; j += kNT * launched)
+        if (j / maxSplit >= nTb || j % maxSplit >= split) atomicStoreAgent(comm->epochs + j, workIndex + 1);
     }
     ev(kEvEnd, 0, 0);
     if (trace != nullptr && tid == 0) {

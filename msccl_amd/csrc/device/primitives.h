@@ -38,6 +38,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t makeRsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7fffffff, 0x00020000);
 }
 
+// Wave-uniform values read from LDS land in VGPRs; readfirstlane moves them to SGPRs so the
+// interpreter state stays out of the vector register budget of the hot loops.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni(uint64_t x) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
 template <int AUX>
 __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);

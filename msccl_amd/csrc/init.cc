@@ -51,13 +51,14 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
   *comm->hostErr = 0;
   NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devAbort, comm->hostAbort, 0), "hipHostGetDevicePointer"));
   NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devErr, comm->hostErr, 0), "hipHostGetDevicePointer"));
-  // flags, then the launch epoch and the done counter on lines of their own
-  const size_t flagWords = (size_t)kFlagSlots * kFlagStride + 2 * kCounterWords;
+  // flags, then one launch-epoch word per workgroup slot
+  const size_t flagWords = (size_t)kFlagSlots * kFlagStride + kFlagSlots;
   NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, flagWords * sizeof(uint64_t)), "hipMalloc flags"));
   NCCLCHECK(hipErr(hipMemset(comm->dFlags, 0, flagWords * sizeof(uint64_t)), "hipMemset"));
-  const uint64_t epoch0 = 1;  // flags start at 0, the first launch waits for epoch 1 (init.cc:300-302)
-  NCCLCHECK(hipErr(hipMemcpy(comm->dFlags + (size_t)kFlagSlots * kFlagStride, &epoch0, sizeof(epoch0),
-                             hipMemcpyHostToDevice), "hipMemcpy epoch"));
+  // flags start at 0, the first launch runs epoch 1 (the reference's workIndex, init.cc:300-302)
+  const std::vector<uint64_t> epoch0(kFlagSlots, 1);
+  NCCLCHECK(hipErr(hipMemcpy(comm->dFlags + (size_t)kFlagSlots * kFlagStride, epoch0.data(),
+                             kFlagSlots * sizeof(uint64_t), hipMemcpyHostToDevice), "hipMemcpy epoch"));
   comm->workIndex = 1;  // flags start at 0 (init.cc:300-302)
   NCCLCHECK(hipErr(hipEventCreateWithFlags(&comm->doneEvent, hipEventDisableTiming), "hipEventCreate"));
   // scratch = max over algorithms of maxBytes * s_chunks / nchunksperloop (init.cc:809-835)
@@ -142,8 +143,8 @@ ncclResult_t commFinish(ncclComm* comm) {
     dc.trace = comm->dTrace;
     dc.traceEvents = comm->traceEvents;
   }
-  dc.epoch = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
-  dc.done = (uint32_t*)(dc.epoch + kCounterWords);
+  dc.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  dc.unused = nullptr;
   NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
   NCCLCHECK(hipErr(hipMemcpy(comm->dComm, &dc, sizeof(dc), hipMemcpyHostToDevice), "hipMemcpy"));
   NCCLCHECK(hipErr(hipDeviceSynchronize(), "hipDeviceSynchronize"));
