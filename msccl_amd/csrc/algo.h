@@ -24,6 +24,11 @@ constexpr int kSliceSteps = kSteps / 4;     // MSCCL_SLICESTEPS
 constexpr int kChunkSteps = kSteps / 2;     // MSCCL_CHUNKSTEPS
 constexpr int kRefWarp = 32;                // reference WARP_SIZE (used only in the chunk math)
 constexpr int kMaxIter = 65536;             // MSCCL_MAX_ITER (msccl_interpreter.h:10)
+// Ring fallback (enqueue.cc:461-476): channels kRingChanBase.. of the connection table carry
+// one ring (send to rank+1, receive from rank-1) each; XML channels are 0..32.
+constexpr int kRingChannels = 8;
+constexpr int kRingChanBase = 40;
+constexpr int kTableChannels = kRingChanBase + kRingChannels;
 
 // Buffer ids (msccl.h:19-21)
 enum BufId : uint8_t { kInput = 0, kOutput = 1, kScratch = 2 };
@@ -31,7 +36,8 @@ enum BufId : uint8_t { kInput = 0, kOutput = 1, kScratch = 2 };
 // Transfer types (msccl.h:23-31)
 enum OpType : uint8_t {
   kSend = 0, kRecv = 1, kRecvCopySend = 2, kRecvReduceSend = 3, kRecvReduceCopy = 4,
-  kRecvReduceCopySend = 5, kLocalCopy = 6, kReduce = 7, kResAdd = 8
+  kRecvReduceCopySend = 5, kLocalCopy = 6, kReduce = 7, kResAdd = 8,
+  kCopySend = 9  // ring AllGather out of place (directCopySend, all_gather.h:59); never from XML
 };
 
 // Protocol ids (devcomm.h:27-29)

@@ -51,6 +51,8 @@ struct ncclComm {
   std::vector<msccl::Algorithm> algos;
   std::vector<msccl::Registration> regs;
   std::vector<msccl::DevAlgoHost> devAlgos;
+  msccl::DevAlgoHost ringAlgos[4];  // ring fallback programs (transport.cc: ringUpload)
+  bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank
   std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
   int maxSplit = 1;                // sub-connections per (channel, peer)
   int coResident = 1;              // ranks of this communicator on this rank's GPU
@@ -60,7 +62,7 @@ struct ncclComm {
   std::vector<uint8_t> sendProtoMask, recvProtoMask;  // bit p = protocol p used
   char* arena = nullptr;
   size_t arenaSize = 0;
-  std::vector<msccl::PeerOffsets> table;              // [32 * nRanks] own table
+  std::vector<msccl::PeerOffsets> table;              // [kTableChannels * nRanks] own table
   std::vector<char*> peerArena;                        // per rank: mapped arena base
   std::vector<bool> peerArenaIpc;                      // opened through hipIpcOpenMemHandle
   msccl::DevSendConn* dSend = nullptr;
@@ -107,6 +109,7 @@ ncclResult_t transportPlan(ncclComm* comm);                 // keys, arena layou
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
                               const std::vector<char*>& peerBases, const std::vector<int>& peerRemote);
 ncclResult_t algoUpload(ncclComm* comm);
+ncclResult_t ringUpload(ncclComm* comm);
 
 // enqueue.cc
 int typeSize(ncclDataType_t t);

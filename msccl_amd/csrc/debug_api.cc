@@ -47,7 +47,14 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
   int idx = selectAlgo(algos, regs, c);
   std::ostringstream o;
   if (idx < 0) {
-    o << "{\"algo\":-1,\"nalgos\":" << algos.size() << "}";
+    o << "{\"algo\":-1,\"nalgos\":" << algos.size();
+    Plan rp;
+    if (envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0 && nranks > 1 && makeRingPlan(c, &rp) == 0)
+      o << ",\"ring\":{\"coll\":" << rp.ringColl << ",\"proto\":" << rp.proto << ",\"channels\":" << rp.ringChannels
+        << ",\"nthreads\":" << rp.refNthreads << ",\"size\":" << rp.count << ",\"dtype\":" << rp.dtype
+        << ",\"nBytes\":" << rp.nBytes << ",\"chunk\":" << rp.chunkSize << ",\"minChunk\":" << rp.minChunk
+        << ",\"lastChunk\":" << rp.ringLastChunk << "}";
+    o << "}";
     return putOut(o.str(), out, outLen);
   }
   Plan p;

@@ -110,6 +110,9 @@ struct DevComm {
   int32_t pad2;
 };
 
+// Ring fallback kinds (RankWork::ringColl)
+enum : int { kRingNone = 0, kRingAllReduce = 1, kRingReduceScatter = 2, kRingAllGather = 3 };
+
 // One rank's share of a launch (the reference passes ncclDevComm* + a 64-B ncclWorkElem,
 // common.h:263-266; here the whole descriptor rides in the kernel argument block).
 struct RankWork {
@@ -129,6 +132,12 @@ struct RankWork {
   uint8_t maxAllowedCount;
   uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
   uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
+  // ring fallback (kRingNone for MSCCL schedules): the program's offsets are chunk / rank indices
+  // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)
+  uint8_t ringColl;
+  int16_t ringRanks;
+  int64_t ringSize;             // elements of one rank's block (args->count)
+  int64_t ringLastChunk;        // LL ReduceScatter / AllGather lastChunkSize (enqueue.cc:653-658)
 };
 
 struct LaunchArgs {

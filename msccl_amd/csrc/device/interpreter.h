@@ -28,7 +28,7 @@
 
 namespace msccl {
 
-enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7 };
+enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7, tCopySend = 9 };
 enum : int { pLL = 0, pLL128 = 1, pSimple = 2 };
 constexpr uint64_t kLLCleanMask = 0x7ffffff8ull;  // NCCL_LL_CLEAN_MASK (devcomm.h:61)
 
@@ -606,24 +606,55 @@ struct Interp {
     bool stop = false;
 
     const int64_t merge = w.merge;
+    // ring fallback mode (w.ringColl != kRingNone): the reference's runRing loop over gridOffset
+    const int ringColl = w.ringColl;
+    const int64_t ringSize = w.ringSize, nr = w.ringRanks, C = w.nBlocks;
     int64_t nelemGrid = 0;
-    for (int64_t grid = 0, iter = 0; grid < sizePer && !stop; grid += nelemGrid, iter++) {
+    for (int64_t grid = 0, iter = 0; grid < (ringColl ? ringSize : sizePer) && !stop; grid += nelemGrid, iter++) {
       int64_t real;
-      if constexpr (PROTO == pSimple) {
+      int64_t ringCo = 0;  // ReduceScatter / AllGather chunkOffset
+      if (ringColl) {
+        const int64_t loop = ringColl == kRingAllReduce ? C * nr * chunkSize : C * chunkSize;
+        const int64_t left = ringSize - grid;
+        if (ringColl == kRingAllReduce) {
+          if constexpr (PROTO == pSimple) {  // all_reduce.h:43-46
+            real = (left + C * nr - 1) / (C * nr);
+            real = real < chunkSize ? real : chunkSize;
+            real = (real + w.minChunk - 1) / w.minChunk * w.minChunk;
+          } else {                           // all_reduce.h:48
+            real = (left + C * nr * w.minChunk - 1) / (C * nr * w.minChunk) * w.minChunk;
+            real = real < chunkSize ? real : chunkSize;
+          }
+        } else {
+          if constexpr (PROTO == pSimple) {  // reduce_scatter.h:33-36, all_gather.h:35-38
+            real = (left + C - 1) / C;
+            real = real < chunkSize ? real : chunkSize;
+            real = (real + w.minChunk - 1) / w.minChunk * w.minChunk;
+          } else {                           // reduce_scatter.h:37-38 (lastChunkSize)
+            real = left < loop ? w.ringLastChunk : chunkSize;
+          }
+        }
+        real = (int)real;
+        ringCo = grid + bid * real;
+        nelemGrid = loop;
+      } else if constexpr (PROTO == pSimple) {
         real = sizePer - grid < chunkSize ? sizePer - grid : chunkSize;
         real = (real + w.minChunk - 1) / w.minChunk * w.minChunk;
       } else {
         int64_t rem = (sizePer - grid + w.minChunk - 1) / w.minChunk * w.minChunk;
         real = rem < chunkSize ? rem : chunkSize;
       }
-      real = (int)real;
-      int nelem = (int)(real < sizePer - grid ? real : sizePer - grid);
-      if (nelem == chunkSize && merge > 1) {
-        // run up to `merge` consecutive full iterations as one (enqueue.cc: makeWork)
-        const int64_t full = (sizePer - grid) / chunkSize;
-        nelem = (int)(chunkSize * (full < merge ? full : merge));
+      int nelem = 0;
+      if (!ringColl) {
+        real = (int)real;
+        nelem = (int)(real < sizePer - grid ? real : sizePer - grid);
+        if (nelem == chunkSize && merge > 1) {
+          // run up to `merge` consecutive full iterations as one (enqueue.cc: makeWork)
+          const int64_t full = (sizePer - grid) / chunkSize;
+          nelem = (int)(chunkSize * (full < merge ? full : merge));
+        }
+        nelemGrid = nelem;
       }
-      nelemGrid = nelem;
       // this workgroup's positions inside every chunk of this iteration (nelem % PE == 0
       // whenever split > 1: the host sets split = 1 otherwise)
       const int Qc = (nelem + PE - 1) / PE;
@@ -655,11 +686,29 @@ struct Interp {
         T* srcP = t.srcbuf == 0 ? thisInput : (t.srcbuf == 1 ? thisOutput : thisScratch);
         T* dstP = t.dstbuf == 0 ? thisInput : (t.dstbuf == 1 ? thisOutput : thisScratch);
         for (int c = 0; c < t.count; c += mac) {
-          const int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
-          const int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;
+          int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
+          int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;
           const int thisCount = mac < t.count - c ? mac : t.count - c;
           Shape s;
           s.n = nelem * thisCount;
+          if (ringColl) {
+            // offsets are chunk indices (AllReduce, all_reduce.h:51-56) or rank indices
+            // (ReduceScatter / AllGather, -1 = chunkOffset alone); nelem = min(real, size - offset)
+            int64_t lim;
+            if (ringColl == kRingAllReduce) {
+              const int64_t ci = t.srcoff >= 0 ? t.srcoff : t.dstoff;
+              if constexpr (PROTO == pSimple) srcoff = grid + bid * nr * real + ci * real;
+              else srcoff = grid + (ci * C + bid) * real;
+              dstoff = srcoff;
+              lim = srcoff;
+            } else {
+              srcoff = ringCo + (t.srcoff >= 0 ? (int64_t)t.srcoff * ringSize : 0);
+              dstoff = ringCo + (t.dstoff >= 0 ? (int64_t)t.dstoff * ringSize : 0);
+              lim = ringCo;
+            }
+            const int64_t ne = ringSize - lim < real ? ringSize - lim : real;
+            s.n = ne > 0 ? (int)ne : 0;
+          }
           if (split == 1) {
             s.Q = (s.n + PE - 1) / PE;
             s.q0 = 0;
@@ -680,6 +729,7 @@ struct Interp {
             case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
             case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
             case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
+            case tCopySend: op<0, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
             case tRe: {
               reduce(srcP, sh->red + t.redPtr, grid + (int64_t)c * sizePer, sizePer, t.numReds, dstP + dstoff, s);
               if (c == 0) step += t.numReds - 1;

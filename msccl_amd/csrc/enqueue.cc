@@ -49,6 +49,7 @@ struct Planned {
   bool memcpyOnly = false;
   size_t copyBytes = 0;
   bool noop = false;
+  bool inPlace = false;
 };
 
 ncclResult_t planOp(const CollOp& op, Planned* out) {
@@ -72,11 +73,18 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   c.rank = comm->rank;
   c.inPlace = inPlaceOf(op.coll, op.sendbuff, op.recvbuff, op.count, op.dtype, comm->rank);
   c.customAlgo = op.customAlgo;
+  out->inPlace = c.inPlace;
   int idx = selectAlgo(comm->algos, comm->regs, c);
   if (idx < 0) {
+    // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
+    if (comm->ringFallback && makeRingPlan(c, &out->plan) == 0) {
+      INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; ring fallback (%s, %d channels)",
+           op.coll, op.count, (int)op.dtype, out->plan.proto == kProtoLL ? "LL" : "Simple", out->plan.ringChannels);
+      return ncclSuccess;
+    }
     WARN("MSCCL: no loaded algorithm matches coll=%d count=%zu type=%d op=%d inplace=%d nranks=%d "
-         "(the reference would fall back to NCCL ring/tree, which this build does not provide)",
-         op.coll, op.count, (int)op.dtype, (int)op.op, (int)c.inPlace, comm->nRanks);
+         "and the ring fallback %s", op.coll, op.count, (int)op.dtype, (int)op.op, (int)c.inPlace, comm->nRanks,
+         comm->ringFallback ? "does not support it" : "is disabled (MSCCL_AMD_RING_FALLBACK=0)");
     return ncclInvalidUsage;
   }
   int protoOverride = -1;
@@ -90,7 +98,37 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   return ncclSuccess;
 }
 
+// Ring fallback: one workgroup per ring channel, the reference's runRing program in ring mode.
+RankWork makeRingWork(Planned& p) {
+  ncclComm* comm = p.op.comm;
+  const int kind = p.plan.ringColl == kRingAllReduce ? 0 : p.plan.ringColl == kRingReduceScatter ? 1
+                   : p.inPlace ? 2 : 3;
+  const DevAlgoHost& da = comm->ringAlgos[kind];
+  RankWork w;
+  memset(&w, 0, sizeof(w));
+  w.sendbuff = p.op.sendbuff;
+  w.recvbuff = p.op.recvbuff;
+  w.scratch = comm->scratch;
+  w.comm = comm->dComm;
+  w.tbs = da.dTbs;
+  w.blob = da.dBlob;
+  w.chunkSize = p.plan.chunkSize;
+  w.minChunk = p.plan.minChunk;
+  w.split = 1;
+  w.merge = 1;
+  w.nBlocks = (int16_t)p.plan.ringChannels;
+  w.refNthreads = (int16_t)p.plan.refNthreads;
+  w.maxAllowedCount = 1;
+  w.ringColl = (uint8_t)p.plan.ringColl;
+  w.ringRanks = (int16_t)comm->nRanks;
+  w.ringSize = p.plan.count;
+  w.ringLastChunk = p.plan.ringLastChunk;
+  w.launchSeq = comm->workIndex++;
+  return w;
+}
+
 RankWork makeWork(Planned& p) {
+  if (p.plan.ringColl) return makeRingWork(p);
   ncclComm* comm = p.op.comm;
   const DevAlgoHost& da = comm->devAlgos[p.plan.algoIndex];
   RankWork w;

@@ -45,6 +45,7 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
   NCCLCHECK(hipErr(hipSetDevice(comm->cudaDev), "hipSetDevice"));
   if (comm->nRanks > 1) NCCLCHECK(loadAlgos(comm));
   comm->timeoutSec = (double)envInt("MSCCL_AMD_TIMEOUT_SEC", 60);
+  comm->ringFallback = envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0;
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostErr, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   *comm->hostAbort = 0;
@@ -228,6 +229,10 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
   hipSetDevice(comm->cudaDev);
   hipDeviceSynchronize();
   for (auto& d : comm->devAlgos) {
+    if (d.dTbs) hipFree(d.dTbs);
+    if (d.dBlob) hipFree(d.dBlob);
+  }
+  for (auto& d : comm->ringAlgos) {
     if (d.dTbs) hipFree(d.dTbs);
     if (d.dBlob) hipFree(d.dBlob);
   }

@@ -184,4 +184,49 @@ int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverri
   return 0;
 }
 
+int makeRingPlan(const CallDesc& c, Plan* p) {
+  *p = Plan();
+  p->algoIndex = -1;
+  if (!(c.redop == 0 || c.redop == 1 || c.redop == 2 || c.redop == 3)) return 5;
+  if (c.coll == kAllReduce) p->ringColl = kRingAllReduce;
+  else if (c.coll == kReduceScatter) p->ringColl = kRingReduceScatter;
+  else if (c.coll == kAllGather) p->ringColl = kRingAllGather;
+  else return 5;
+  argsCheck(c, &p->count, &p->dtype, &p->nBytes);   // AllGather: bytes, int8 (argcheck.cc:44-51)
+  const int ts = refTypeSize(p->dtype);
+  const bool llOk = protoEnabled(kProtoLL), simpleOk = protoEnabled(kProtoSimple);
+  if (!llOk && !simpleOk) return 5;
+  p->proto = (llOk && (p->nBytes <= (512 << 10) || !simpleOk)) ? kProtoLL : kProtoSimple;
+  const int64_t forced = envInt("MSCCL_AMD_RING_CHANNELS", 0);
+  int64_t ch = forced > 0 ? forced : std::max<int64_t>(1, p->nBytes >> 18);
+  p->ringChannels = (int)std::max<int64_t>(1, std::min<int64_t>(kRingChannels, ch));
+  const int64_t bs[3] = {envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16),
+                         envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8), envInt("NCCL_BUFFSIZE", 1 << 22)};
+  int nt;
+  if (p->proto == kProtoLL) {
+    nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512);
+    p->chunkSize = bs[0] / kFifoSteps / 2 / ts;             // calcBytePerStep (primitives.h:49-51)
+    p->minChunk = (int64_t)nt * 8 / ts;                      // all_reduce.h:30-31
+  } else {
+    nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512) + kRefWarp;  // enqueue.cc:516-517
+    p->chunkSize = bs[2] / kFifoSteps / ts * kChunkSteps;   // x ALLREDUCE/REDUCESCATTER/ALLGATHER_CHUNKSTEPS
+    p->minChunk = (int64_t)(nt - kRefWarp) * 8 / ts;         // all_reduce.h:45 rounding unit
+  }
+  p->refNthreads = nt;
+  p->maxAllowedCount = 1;
+  p->sizeMultiplier = 1;
+  if (p->proto == kProtoLL && p->ringColl != kRingAllReduce) {
+    // enqueue.cc:653-658 with nchunksPerLoop = nRanks (ring pattern)
+    const int64_t stepSize = bs[0] / kFifoSteps;
+    const int64_t sliceSize = stepSize * 8 / 16;
+    const int64_t loop = (int64_t)p->ringChannels * c.nRanks * sliceSize;
+    int64_t last = (p->nBytes - (p->nBytes / loop) * loop + (int64_t)p->ringChannels * c.nRanks - 1) /
+                   ((int64_t)p->ringChannels * c.nRanks);
+    const int64_t align = (int64_t)nt * 8;
+    last = (last + align - 1) / align * align;
+    p->ringLastChunk = last / ts;
+  }
+  return 0;
+}
+
 }  // namespace msccl

@@ -41,6 +41,10 @@ struct Plan {
   int64_t minChunk = 0;     // LL: nthreads*8/ts; Simple: (nthreads-32)*8/ts
   size_t scratchNeeded = 0;
   int nIters = 0;
+  // ring fallback (algoIndex == -1): kRingAllReduce / kRingReduceScatter / kRingAllGather
+  int ringColl = 0;
+  int ringChannels = 0;
+  int64_t ringLastChunk = 0;  // LL ReduceScatter / AllGather lastChunkSize (elements)
 };
 
 int refTypeSize(int dtype);
@@ -54,6 +58,12 @@ int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverri
 // keeps the GPU's workgroups within MSCCL_AMD_TARGET_WGS (default 256 = one per CU).
 // MSCCL_AMD_SPLIT forces a value.  Every rank must compute the same value.
 int chooseSplit(int maxBlocks, int coResident);
+// The reference's fallback when no MSCCL algorithm matches (enqueue.cc:461-476): a ring
+// AllReduce / ReduceScatter / AllGather (collectives/device/all_reduce.h:14-100,
+// reduce_scatter.h:13-67, all_gather.h:13-78).  Fills *p (algoIndex -1, ringColl set) and returns
+// 0, or returns ncclInvalidUsage when the collective / op has no ring (AllToAll, custom, Avg).
+// Channels, protocol and thread count are this build's choice (oracle/ring.py: ring_params).
+int makeRingPlan(const CallDesc& c, Plan* p);
 // NCCL_ALGO / NCCL_PROTO gates
 bool mscclEnabled();
 bool protoEnabled(int proto);

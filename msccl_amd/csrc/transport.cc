@@ -63,6 +63,15 @@ ncclResult_t transportPlan(ncclComm* comm) {
       }
     }
   }
+  // ring fallback connections: one ring per channel kRingChanBase + c (send to rank+1, receive
+  // from rank-1), LL and Simple FIFOs, one sub-connection each (the ring runs unsplit)
+  if (comm->ringFallback && n > 1) {
+    const uint8_t bits = (uint8_t)((1u << kProtoLL) | (1u << kProtoSimple));
+    for (int c = 0; c < kRingChannels; c++) {
+      sends[ConnKey{kRingChanBase + c, (comm->rank + 1) % n}] |= bits;
+      recvs[ConnKey{kRingChanBase + c, (comm->rank + n - 1) % n}] |= bits;
+    }
+  }
   comm->sendKeys.clear();
   comm->recvKeys.clear();
   comm->sendProtoMask.clear();
@@ -73,22 +82,29 @@ ncclResult_t transportPlan(ncclComm* comm) {
   const int S = comm->maxSplit;
   const int64_t llBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->llSlotLines * 16, kFifoAlign);
   const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
-  comm->table.assign((size_t)kMaxChannels * n, PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
+  comm->table.assign((size_t)kTableChannels * n, PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
+  // ring keys have a single sub-connection: stride 0 makes every sub alias sub 0
+  auto subsOf = [&](const ConnKey& k) { return k.chan >= kRingChanBase ? 1 : S; };
+  for (int c = kRingChanBase; c < kTableChannels; c++)
+    for (int p = 0; p < n; p++) {
+      PeerOffsets& po = comm->table[(size_t)c * n + p];
+      po.llStride = po.simpleStride = po.wordStride = 0;
+    }
   size_t off = 0;
-  for (auto& k : comm->sendKeys) { comm->table[(size_t)k.chan * n + k.peer].sendHead = (int64_t)off; off += kWordStride * S; }
-  for (auto& k : comm->recvKeys) { comm->table[(size_t)k.chan * n + k.peer].recvTail = (int64_t)off; off += kWordStride * S; }
+  for (auto& k : comm->sendKeys) { comm->table[(size_t)k.chan * n + k.peer].sendHead = (int64_t)off; off += kWordStride * subsOf(k); }
+  for (auto& k : comm->recvKeys) { comm->table[(size_t)k.chan * n + k.peer].recvTail = (int64_t)off; off += kWordStride * subsOf(k); }
   off = alignUp(off, kFifoAlign);
   for (size_t i = 0; i < comm->recvKeys.size(); i++) {
     auto& k = comm->recvKeys[i];
     PeerOffsets& po = comm->table[(size_t)k.chan * n + k.peer];
-    // LL128 schedules run on the LL FIFO format in this build
+    // LL and LL128 share the LL FIFO memory (two line formats)
     if (comm->recvProtoMask[i] & ((1u << kProtoLL) | (1u << kProtoLL128))) {
       po.recvLL = (int64_t)off;
-      off += (size_t)llBytes * S;
+      off += (size_t)llBytes * subsOf(k);
     }
     if (comm->recvProtoMask[i] & (1u << kProtoSimple)) {
       po.recvSimple = (int64_t)off;
-      off += (size_t)simpleBytes * S;
+      off += (size_t)simpleBytes * subsOf(k);
     }
   }
   comm->arenaSize = off ? off : kFifoAlign;
@@ -167,6 +183,91 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
   return ncclSuccess;
 }
 
+// The reference's ring collectives as programs of this interpreter, one thread block per ring
+// channel.  Offsets are indices, resolved per iteration by the kernel's ring mode:
+//   AllReduce: chunk index c of calcOffset(c) (all_reduce.h:51-98);
+//   ReduceScatter / AllGather: rank index d of chunkOffset + d * size, -1 = chunkOffset alone
+//   (reduce_scatter.h:50-65, all_gather.h:52-75).
+// Kinds: 0 AllReduce, 1 ReduceScatter, 2 AllGather in place, 3 AllGather out of place.
+static std::vector<Transfer> ringProgram(int kind, int r, int n) {
+  std::vector<Transfer> v;
+  auto add = [&](uint8_t type, uint8_t sb, int so, uint8_t db, int dof) {
+    Transfer t;
+    t.type = type;
+    t.srcbuf = sb;
+    t.srcoff = (int16_t)so;
+    t.dstbuf = db;
+    t.dstoff = (int16_t)dof;
+    t.count = 1;
+    v.push_back(t);
+  };
+  auto ring = [&](int k) { return (r + k) % n; };  // devUserRanks of the rank-order ring
+  if (kind == 0) {
+    add(kSend, kInput, ring(n - 1), kInput, -1);
+    for (int j = 2; j < n; j++) add(kRecvReduceSend, kInput, ring(n - j), kInput, -1);
+    add(kRecvReduceCopySend, kInput, ring(0), kOutput, ring(0));
+    for (int j = 1; j < n - 1; j++) add(kRecvCopySend, kInput, -1, kOutput, ring(n - j));
+    add(kRecv, kInput, -1, kOutput, ring(1));
+  } else if (kind == 1) {
+    add(kSend, kInput, ring(n - 1), kInput, -1);
+    for (int j = 2; j < n; j++) add(kRecvReduceSend, kInput, ring(n - j), kInput, -1);
+    add(kRecvReduceCopy, kInput, ring(0), kOutput, -1);
+  } else {
+    if (kind == 2) add(kSend, kOutput, ring(0), kOutput, -1);  // directSend from the output
+    else add(kCopySend, kInput, -1, kOutput, ring(0));          // directCopySend
+    for (int j = 1; j < n - 1; j++) add(kRecvCopySend, kInput, -1, kOutput, ring(n - j));
+    add(kRecv, kInput, -1, kOutput, ring(1));
+  }
+  return v;
+}
+
+ncclResult_t ringUpload(ncclComm* comm) {
+  const int n = comm->nRanks;
+  if (!comm->ringFallback || n < 2) return ncclSuccess;
+  int sendIdx[kRingChannels], recvIdx[kRingChannels];
+  for (int c = 0; c < kRingChannels; c++) {
+    sendIdx[c] = recvIdx[c] = -1;
+    for (size_t i = 0; i < comm->sendKeys.size(); i++)
+      if (comm->sendKeys[i] == ConnKey{kRingChanBase + c, (comm->rank + 1) % n}) sendIdx[c] = (int)i;
+    for (size_t i = 0; i < comm->recvKeys.size(); i++)
+      if (comm->recvKeys[i] == ConnKey{kRingChanBase + c, (comm->rank + n - 1) % n}) recvIdx[c] = (int)i;
+    if (sendIdx[c] < 0 || recvIdx[c] < 0) return ncclInternalError;
+  }
+  for (int kind = 0; kind < 4; kind++) {
+    const std::vector<Transfer> prog = ringProgram(kind, comm->rank, n);
+    std::vector<DevTbHeader> hdr(kRingChannels);
+    std::vector<char> blob;
+    for (const Transfer& t : prog) {
+      DevTransfer x;
+      memset(&x, 0, sizeof(x));
+      x.srcoff = t.srcoff;
+      x.dstoff = t.dstoff;
+      x.srcbuf = t.srcbuf;
+      x.dstbuf = t.dstbuf;
+      x.type = t.type;
+      x.count = t.count;
+      const char* p = (const char*)&x;
+      blob.insert(blob.end(), p, p + sizeof(x));
+    }
+    blob.resize(alignUp(blob.size() + 16, 16));
+    for (int c = 0; c < kRingChannels; c++) {  // every channel runs the same program
+      DevTbHeader& h = hdr[c];
+      memset(&h, 0, sizeof(h));
+      h.sendConn = (int16_t)sendIdx[c];
+      h.recvConn = (int16_t)recvIdx[c];
+      h.nsteps = (uint16_t)prog.size();
+      h.blobOffset = 0;
+    }
+    DevAlgoHost& d = comm->ringAlgos[kind];
+    d.nBlocks = kRingChannels;
+    if (hipMalloc(&d.dTbs, hdr.size() * sizeof(DevTbHeader)) != hipSuccess) return ncclUnhandledCudaError;
+    if (hipMalloc(&d.dBlob, blob.size()) != hipSuccess) return ncclUnhandledCudaError;
+    hipMemcpy(d.dTbs, hdr.data(), hdr.size() * sizeof(DevTbHeader), hipMemcpyHostToDevice);
+    hipMemcpy(d.dBlob, blob.data(), blob.size(), hipMemcpyHostToDevice);
+  }
+  return ncclSuccess;
+}
+
 // Pack every algorithm's per-tb programs and upload them (replaces the 29 MB
 // mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 ncclResult_t algoUpload(ncclComm* comm) {
@@ -223,7 +324,7 @@ ncclResult_t algoUpload(ncclComm* comm) {
     hipMemcpy(d.dBlob, blob.data(), blob.size(), hipMemcpyHostToDevice);
     comm->devAlgos.push_back(d);
   }
-  return ncclSuccess;
+  return ringUpload(comm);
 }
 
 }  // namespace msccl

@@ -143,3 +143,71 @@ def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, o
     if coll == L.ALLGATHER:
         res = [r.view(N.storage(dt)) for r in res]
     return gpu, [np.asarray(r) for r in res], ins
+
+
+def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, in_place: bool = True,
+                      seed: int = 1, mode: str = "uniform", iters: int = 1):
+    """No MSCCL schedule loaded: every call takes the ring fallback (enqueue.cc:461-476).
+    Returns (gpu_outputs, oracle_outputs, ring_params) compared by the caller."""
+    import torch
+    from oracle import ring as R
+    os.environ.pop("MSCCL_XML_FILES", None)
+    os.environ.pop("MSCCL_CONFIG", None)
+    dev = torch.device("cuda:0")
+    comms = M.Comm.init_all([0] * nranks)
+    try:
+        if coll == L.ALLREDUCE:
+            in_n, out_n = count, count
+        elif coll == L.REDUCE_SCATTER:
+            in_n, out_n = count * nranks, count
+        else:
+            in_n, out_n = count, count * nranks
+        ins = gen_inputs(nranks, in_n, dt, seed, mode)
+        t_in = [to_torch(x, dev) for x in ins]
+        if in_place:
+            if coll == L.ALLREDUCE:
+                t_out, sends, recvs = t_in, [t.data_ptr() for t in t_in], [t.data_ptr() for t in t_in]
+            elif coll == L.REDUCE_SCATTER:
+                t_out = [t[r * count:(r + 1) * count] for r, t in enumerate(t_in)]
+                sends, recvs = [t.data_ptr() for t in t_in], [t.data_ptr() for t in t_out]
+            else:
+                t_out = [torch.zeros(out_n, dtype=t_in[0].dtype, device=dev) for _ in range(nranks)]
+                for r in range(nranks):
+                    t_out[r][r * count:(r + 1) * count] = t_in[r]
+                sends = [t_out[r][r * count:(r + 1) * count].data_ptr() for r in range(nranks)]
+                recvs = [t.data_ptr() for t in t_out]
+        else:
+            t_out = [torch.full((out_n,), 7, dtype=t_in[0].dtype, device=dev) for _ in range(nranks)]
+            sends, recvs = [t.data_ptr() for t in t_in], [t.data_ptr() for t in t_out]
+        torch.cuda.synchronize()
+        stream = torch.cuda.current_stream().cuda_stream
+        for _ in range(iters):
+            with M.group():
+                for r, c in enumerate(comms):
+                    if coll == L.ALLREDUCE:
+                        c.all_reduce(sends[r], recvs[r], count, dt, op, stream)
+                    elif coll == L.REDUCE_SCATTER:
+                        c.reduce_scatter(sends[r], recvs[r], count, dt, op, stream)
+                    else:
+                        c.all_gather(sends[r], recvs[r], count, dt, stream)
+        torch.cuda.synchronize()
+        for c in comms:
+            if c.async_error() != 0:
+                raise M.NcclError(c.async_error(), "kernel (async error)")
+        gpu = [from_torch(t, N.storage(dt)) for t in t_out]
+    finally:
+        for c in comms:
+            c.destroy()
+    o_in = [x.copy() for x in ins]
+    if coll == L.ALLGATHER:
+        o_out = [np.zeros(out_n, N.storage(dt)) for _ in range(nranks)]
+    elif in_place:
+        o_out = [None] * nranks
+    else:
+        o_out = [np.full(out_n, 7, N.storage(dt)) for _ in range(nranks)]
+    res = None
+    for _ in range(iters):
+        res, rp = R.run(coll, count, dt, op, o_in, o_out, in_place)
+        if iters > 1 and coll == L.ALLREDUCE and in_place:
+            o_in = res
+    return gpu, [np.asarray(r) for r in res], rp

@@ -88,11 +88,14 @@ def test_single_rank_is_a_copy():
         comm.destroy()
 
 
-def test_no_matching_algorithm_and_zero_count(tmp_path):
+def test_no_matching_algorithm_and_zero_count(tmp_path, monkeypatch):
+    """With the ring fallback disabled (MSCCL_AMD_RING_FALLBACK=0) a call no XML matches is an
+    error; test_no_match_falls_back_to_ring covers the default."""
     import torch
     p = tmp_path / "ap.xml"
     p.write_text(xmlgen.allreduce_allpairs(2, 4, "LL", max_bytes=1 << 20))
     os.environ["MSCCL_XML_FILES"] = str(p)
+    monkeypatch.setenv("MSCCL_AMD_RING_FALLBACK", "0")
     comms = M.Comm.init_all([0, 0])
     try:
         a = [torch.zeros(1 << 20, device="cuda") for _ in comms]
@@ -110,6 +113,35 @@ def test_no_matching_algorithm_and_zero_count(tmp_path):
         torch.cuda.synchronize()
         info = comms[0].info()
         assert info["nranks"] == 2 and info["sendConns"] == 4 and info["recvConns"] == 4
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def test_no_match_falls_back_to_ring(tmp_path):
+    """The reference falls back to its ring when no MSCCL algorithm matches (enqueue.cc:461-476):
+    not divisible by nchunksperloop, beyond maxBytes, out of place against an in-place XML; the
+    MSCCL schedule still serves the calls it matches, on the same communicators."""
+    import torch
+    p = tmp_path / "ap.xml"
+    p.write_text(xmlgen.allreduce_allpairs(2, 4, "LL", max_bytes=1 << 20))
+    os.environ["MSCCL_XML_FILES"] = str(p)
+    comms = M.Comm.init_all([0, 0])
+    try:
+        g = torch.Generator().manual_seed(11)
+        s = torch.cuda.current_stream().cuda_stream
+        for count, inplace in [(24, True), (1 << 19, True), (4096, False), (4096, True), (1001, False)]:
+            x = [torch.randint(-4, 5, (count,), generator=g).float() for _ in comms]
+            d = [t.cuda() for t in x]
+            o = d if inplace else [torch.zeros_like(t) for t in d]
+            with M.group():
+                for c, a, b in zip(comms, d, o):
+                    c.all_reduce(a.data_ptr(), b.data_ptr(), count, M.FLOAT32, M.SUM, s)
+            torch.cuda.synchronize()
+            for b in o:
+                assert torch.equal(b.cpu(), x[0] + x[1]), (count, inplace)
+        assert all(c.async_error() == 0 for c in comms)
+        assert comms[0].info()["sendConns"] == 4 + 8   # 4 all-pairs channels + 8 ring channels
     finally:
         for c in comms:
             c.destroy()

@@ -1,0 +1,49 @@
+"""Build-time resource check of the gfx950 kernels (no GPU needed).
+
+The Makefile keeps hipcc's `-Rpass-analysis=kernel-resource-usage` report next to every kernel
+object (build/obj/device/*.res).  The LL and Simple interpreter kernels of the floating-point
+types the benchmarks and the reference's configs use must run without scratch: a spill inside the
+FIFO loops is a private-memory round trip per pack, and it cost 10-20 % of LL bandwidth when the
+fp16 kernel once needed 1.6 KiB of scratch per lane.  VGPRs must stay <= 128 so that two
+512-thread workgroups fit each CU (the schedules' workgroups spin on each other and must all be
+resident: __launch_bounds__(512, 4)).
+"""
+import glob
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RES = os.path.join(ROOT, "build", "obj", "device")
+
+# mangled element types: f = float, DF16_ = _Float16, NS_4Bf16E = bf16; protocol 0 = LL, 2 = Simple
+HOT = re.compile(r"mscclKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi[02]EE")
+
+
+def _kernels():
+    out = {}
+    for f in glob.glob(os.path.join(RES, "*.res")):
+        name = None
+        for line in open(f):
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name = m.group(1)
+                out[name] = {}
+                continue
+            m = re.search(r"(VGPRs|ScratchSize \[bytes/lane\]): (\d+)", line)
+            if m and name:
+                out[name]["vgpr" if m.group(1) == "VGPRs" else "scratch"] = int(m.group(2))
+    return out
+
+
+def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
+    ks = _kernels()
+    if not ks:
+        pytest.skip("no kernel resource reports (run __graft_entry__.build() first)")
+    hot = {k: v for k, v in ks.items() if HOT.search(k)}
+    assert len(hot) == 3 * 4 * 2, sorted(hot)
+    for k, v in hot.items():
+        assert v.get("scratch", 1) == 0, (k, v)
+    for k, v in ks.items():
+        assert v.get("vgpr", 999) <= 128, (k, v)

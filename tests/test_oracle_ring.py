@@ -1,0 +1,78 @@
+"""The ring-fallback oracle (oracle/ring.py) against exact sums, and the product's ring plan
+(plan.cc makeRingPlan via mscclAmdPlanJson) against the oracle's ring_params (CPU only)."""
+import numpy as np
+import pytest
+
+import msccl_amd as M
+from msccl_amd import xmlgen
+from oracle import loader as L
+from oracle import ring as R
+
+
+@pytest.mark.parametrize("n", [2, 3, 5, 8])
+@pytest.mark.parametrize("count", [1, 7, 1000, 70001, 300001])
+def test_ring_oracle_exact(n, count):
+    rng = np.random.default_rng(count + n)
+    ins = [rng.integers(-4, 5, count).astype(np.float32) for _ in range(n)]
+    want = np.sum(np.stack(ins).astype(np.float64), axis=0)
+    outs, _ = R.run(L.ALLREDUCE, count, 7, 0, [x.copy() for x in ins], [None] * n, True)
+    for o in outs:
+        assert np.array_equal(o.astype(np.float64), want)
+    big = [rng.integers(-4, 5, count * n).astype(np.float32) for _ in range(n)]
+    tot = np.sum(np.stack(big), axis=0)
+    outs, _ = R.run(L.REDUCE_SCATTER, count, 7, 0, [x.copy() for x in big], [None] * n, True)
+    for r, o in enumerate(outs):
+        assert np.array_equal(o, tot[r * count:(r + 1) * count])
+    cat = np.concatenate([x[:count] for x in big])
+    for ip in (True, False):
+        outs, _ = R.run(L.ALLGATHER, count, 7, 0, [x[:count].copy() for x in big],
+                        [np.zeros(count * n, np.float32) for _ in range(n)], ip)
+        for o in outs:
+            assert np.array_equal(o, cat)
+
+
+def test_ring_oracle_association_order():
+    """fp32 values whose sum depends on the order: the oracle follows the ring (chunk c starts at
+    rank c+1, recv-reduce fn(peer, local) in LL), not a left fold."""
+    n, count = 3, 3 * 1024
+    ins = [np.full(count, v, np.float32) for v in (1e8, 1.0, -1e8)]
+    outs, rp = R.run(L.ALLREDUCE, count, 7, 0, [x.copy() for x in ins], [None] * n, True)
+    assert rp["proto"] == L.PROTO_LL
+    vals = set(np.unique(outs[0]).tolist())
+    assert vals <= {0.0, 1.0} and len(vals) == 2
+
+
+CASES = [(L.ALLREDUCE, c, dt) for c in (1, 999, 1 << 16, 131073, 1 << 22, 50000001) for dt in (7, 6, 9, 0)] + \
+        [(L.REDUCE_SCATTER, c, dt) for c in (1, 4097, 1 << 18, 3000001) for dt in (7, 9)] + \
+        [(L.ALLGATHER, c, dt) for c in (1, 4097, 1 << 18, 3000001) for dt in (7, 6)]
+
+
+@pytest.mark.parametrize("n", [2, 8])
+@pytest.mark.parametrize("coll,count,dt", CASES)
+def test_ring_plan_matches_oracle(tmp_path, n, coll, count, dt):
+    p = tmp_path / "none.xml"
+    p.write_text(xmlgen.allreduce_allpairs(n, 1, "LL", max_bytes=1))  # matches nothing
+    prod = M.plan_json(str(p), 0, n, coll, count, dt, 0, coll != L.ALLGATHER)
+    assert prod["algo"] == -1
+    rp = R.ring_params(coll, count, dt, n)
+    ring = prod["ring"]
+    assert (ring["proto"], ring["channels"], ring["nthreads"], ring["size"], ring["dtype"], ring["nBytes"],
+            ring["chunk"], ring["minChunk"], ring["lastChunk"]) == \
+        (rp["proto"], rp["channels"], rp["nthreads"], rp["size"], rp["dtype"], rp["nbytes"], rp["chunk"],
+         rp["min_chunk"], rp["last_chunk"])
+
+
+def test_ring_plan_env(tmp_path, monkeypatch):
+    p = tmp_path / "none.xml"
+    p.write_text(xmlgen.allreduce_allpairs(2, 1, "LL", max_bytes=1))
+    monkeypatch.setenv("MSCCL_AMD_RING_CHANNELS", "5")
+    monkeypatch.setenv("NCCL_PROTO", "Simple")
+    prod = M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 0, True)["ring"]
+    rp = R.ring_params(L.ALLREDUCE, 1000, 7, 2)
+    assert prod["channels"] == rp["channels"] == 5
+    assert prod["proto"] == rp["proto"] == L.PROTO_SIMPLE
+    monkeypatch.setenv("MSCCL_AMD_RING_FALLBACK", "0")
+    assert "ring" not in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 0, True)
+    # Avg has no ring in this build (PreMulSum/SumPostDiv are not provided)
+    monkeypatch.delenv("MSCCL_AMD_RING_FALLBACK")
+    assert "ring" not in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 4, True)
