@@ -419,13 +419,14 @@ def measure_e2e(comms, n, nbytes, dt, ts, stream, dev):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
-        for i in range(n):
-            dbufs[i].copy_(host_in[i], non_blocking=True)
-        with M.group():
-            for c, b in zip(comms, dbufs):
-                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
-        for i in range(n):
-            host_out[i].copy_(dbufs[i], non_blocking=True)
+        with torch.cuda.stream(stream):   # copies and the collective ordered on one stream
+            for i in range(n):
+                dbufs[i].copy_(host_in[i], non_blocking=True)
+            with M.group():
+                for c, b in zip(comms, dbufs):
+                    c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+            for i in range(n):
+                host_out[i].copy_(dbufs[i], non_blocking=True)
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / reps
     algbw = nbytes / t / 1e9
