@@ -685,10 +685,15 @@ struct Interp {
         }
         T* srcP = t.srcbuf == 0 ? thisInput : (t.srcbuf == 1 ? thisOutput : thisScratch);
         T* dstP = t.dstbuf == 0 ? thisInput : (t.dstbuf == 1 ? thisOutput : thisScratch);
-        for (int c = 0; c < t.count; c += mac) {
+        // maxAllowedCount keeps one reference primitive call within one FIFO step
+        // (enqueue.cc:700-711); these primitives cut calls into FIFO steps themselves, so when the
+        // iteration covers whole chunks (consecutive chunks are contiguous) a transfer's chunks
+        // move as one call.  Not for `re`: its per-element path depends on the call's size.
+        const int macT = (t.type != tRe && !ringColl && nelem == sizePer) ? t.count : mac;
+        for (int c = 0; c < t.count; c += macT) {
           int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
           int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;
-          const int thisCount = mac < t.count - c ? mac : t.count - c;
+          const int thisCount = macT < t.count - c ? macT : t.count - c;
           Shape s;
           s.n = nelem * thisCount;
           if (ringColl) {

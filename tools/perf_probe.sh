@@ -4,15 +4,10 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 probe() {
   echo "== $*"
-  timeout -k 10 120 env "$@" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print([ (s['bytes'], s['busbw']) for s in d['sweep']], d['roofline']['achieved'])" || exit 1
+  timeout -k 10 120 env "$@" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print([ (s['bytes'], s['busbw'], s['kernel_ms']) for s in d['sweep']], d['roofline']['achieved'])" || exit 1
 }
-B="python bench.py --no-cpu --quiet --steps 40 --warmup 10 --sizes 1048576,8388608,33554432"
+B="python bench.py --no-cpu --quiet --steps 40 --warmup 10 --sizes 65536,1048576,4194304,8388608,16777216,33554432"
 for pass in 1 2; do
 probe X=1 $B --instances 16
-probe X=1 $B --instances 32
-probe X=1 $B --instances 16 --proto LL128
-probe MSCCL_AMD_MERGE=4 $B --instances 16 --proto LL128
 probe X=1 $B --instances 16 --proto Simple
-probe MSCCL_AMD_MERGE=4 $B --instances 16 --proto Simple
-probe X=1 $B --instances 8 --proto Simple
 done
