@@ -44,6 +44,7 @@ def parse():
     ap.add_argument("--proto", default="LL")
     ap.add_argument("--dtype", default=None)
     ap.add_argument("--instances", type=int, default=0, help="all-pairs instances for large sizes (0 = auto)")
+    ap.add_argument("--tiers", default=None, help="schedule tiers lo:hi:instances,... (default: see make_xmls)")
     ap.add_argument("--sizes", default=None, help="comma list of bytes (default 128B..32MiB)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -83,17 +84,32 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int):
     return hbm, wire
 
 
-def make_xmls(n: int, proto: str, inst_large: int, tmp: str):
-    """Small sizes: 1 instance (ncpl = n*n, smallest divisibility); large: inst_large instances."""
-    ncpl_small = n * n
-    thresh = 64 << 10
-    small = xmlgen.allreduce_allpairs(n, 1, proto, True, 0, thresh, name="allpairs_small")
-    large = xmlgen.allreduce_allpairs(n, inst_large, proto, True, thresh, (1 << 30) + 1, name="allpairs_large")
-    ps = os.path.join(tmp, "bench_ap%d_%s_small_%d.xml" % (n, proto, os.getpid()))
-    pl = os.path.join(tmp, "bench_ap%d_%s_i%d_%d.xml" % (n, proto, inst_large, os.getpid()))
-    open(ps, "w").write(small)
-    open(pl, "w").write(large)
-    return [ps, pl], ncpl_small, inst_large * n * n, thresh
+def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
+    """The all-pairs schedule in size tiers, as a user registers several msccl-tools XMLs with
+    minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path)].  Few instances
+    keep small messages divisible and latency-light; 8 instances suit 2-8 MiB on one GPU; the
+    large tier uses inst_large.  At 8 ranks: 1 instance below 64 KiB, inst_large above."""
+    if tiers_arg:
+        spec = [tuple(int(v) for v in t.split(":")) for t in tiers_arg.split(",")]
+    elif n <= 2:
+        spec = [(0, 4 << 10, 1), (4 << 10, 2 << 20, inst_large), (2 << 20, 8 << 20, 8),
+                (8 << 20, (1 << 30) + 1, inst_large)]
+    else:
+        spec = [(0, 64 << 10, 1), (64 << 10, (1 << 30) + 1, inst_large)]
+    tiers = []
+    for k, (lo, hi, inst) in enumerate(spec):
+        x = xmlgen.allreduce_allpairs(n, inst, proto, True, lo, hi, name="allpairs_t%d_i%d" % (k, inst))
+        pth = os.path.join(tmp, "bench_ap%d_%s_t%d_i%d_%d.xml" % (n, proto, k, inst, os.getpid()))
+        open(pth, "w").write(x)
+        tiers.append((lo, hi, inst, pth))
+    return tiers
+
+
+def tier_of(tiers, nbytes):
+    for t in tiers:
+        if t[0] <= nbytes < t[1]:
+            return t
+    raise ValueError("no schedule tier for %d bytes" % nbytes)
 
 
 def cpu_baseline(n: int, nbytes: int, dt: int, seconds: float):
@@ -263,8 +279,8 @@ def main():
     inst = a.instances or (16 if n <= 2 else (8 if n <= 4 else 4))
     sizes = [int(s) for s in a.sizes.split(",")] if a.sizes else SIZES
     tmp = os.environ.get("TMPDIR", "/tmp")
-    xmls, ncpl_small, ncpl_large, thresh = make_xmls(n, a.proto, inst, tmp)
-    os.environ["MSCCL_XML_FILES"] = ":".join(xmls)
+    tiers = make_xmls(n, a.proto, inst, tmp, a.tiers)
+    os.environ["MSCCL_XML_FILES"] = ":".join(t[3] for t in tiers)
     os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "30")
 
     if multi:
@@ -286,8 +302,7 @@ def main():
     stream.wait_stream(torch.cuda.current_stream(devs[0]))
     maxb = max(sizes)
     bufs = [torch.empty(maxb // 4 + 64, dtype=torch.float32, device=d).uniform_(-1, 1) for d in devs]
-    algo_large = M.algo_json(xmls[1], my_ranks[0], n)
-    algo_small = M.algo_json(xmls[0], my_ranks[0], n)
+    algos = {t[3]: M.algo_json(t[3], my_ranks[0], n) for t in tiers}
 
     def one_step(nbytes):
         cnt = nbytes // ts
@@ -299,7 +314,8 @@ def main():
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for nbytes in sizes:
         cnt = nbytes // ts
-        ncpl = ncpl_small if nbytes < thresh else ncpl_large
+        tier = tier_of(tiers, nbytes)
+        ncpl = tier[2] * n * n
         if cnt % ncpl:
             continue
         for _ in range(a.warmup):
@@ -337,7 +353,7 @@ def main():
                 raise RuntimeError("kernel reported an error (timeout/abort) at %d bytes" % nbytes)
         algbw = nbytes / t / 1e9
         bus = algbw * 2 * (n - 1) / n
-        algo = algo_small if nbytes < thresh else algo_large
+        algo = algos[tier[3]]
         size_per = cnt // ncpl
         hbm, wire = schedule_bytes(algo, size_per, ts, proto_id)
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
@@ -389,6 +405,7 @@ def main():
         "config": {"workload": workload,
                    "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
+                   "tiers": [[t[0], t[1], t[2]] for t in tiers],
                    "launch": "hipgraph" if a.graph else "eager",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
