@@ -196,7 +196,13 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         open(pth, "w").write(x)
         paths.append(pth)
     os.environ["MSCCL_XML_FILES"] = ":".join(paths)
+
+    def note(msg):
+        if rank == 0 and not a.quiet:
+            print("# %s: %s" % (cfg, msg), file=sys.stderr, flush=True)
+    note("init %d ranks" % n)
     comms = init_comms(multi, world, rank, n)
+    note("init done")
     ts = M.TYPE_SIZE[dt]
     stream = torch.cuda.Stream(dev)
     nloc = len(comms)
@@ -229,6 +235,7 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         res = {}
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for name, (fn, busbytes) in phases.items():
+            note("%s warmup" % name)
             for _ in range(max(1, a.warmup)):
                 fn()
             if multi:
@@ -253,6 +260,7 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 raise RuntimeError("kernel reported an error (timeout/abort)")
             res[name] = {"ms": round(t * 1e3, 4), "kernel_ms": round(ev_ms, 4),
                          "busbw": round(busbytes / t / 1e9, 3), "steps": k}
+            note("%s %.3f ms, busbw %.1f GB/s" % (name, t * 1e3, busbytes / t / 1e9))
         res["bytes"] = S
         res["dtype"] = {M.BFLOAT16: "bf16", M.FLOAT32: "f32"}[dt]
         res["ranks"] = n
@@ -285,6 +293,9 @@ def main():
 
     if multi:
         import torch.distributed as dist
+        # MSCCL_AMD_BENCH_ONE_GPU=1 puts every rank on cuda:0: rehearses the multi-process path
+        # (bootstrap, hipIpc FIFOs, barriers, max over ranks) on a one-GPU box
+        local = 0 if os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") == "1" else local
         torch.cuda.set_device(local)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         devs = [torch.device("cuda", local)]

@@ -53,7 +53,8 @@ struct ncclComm {
   std::vector<msccl::DevAlgoHost> devAlgos;
   msccl::DevAlgoHost ringAlgos[4];  // ring fallback programs (transport.cc: ringUpload)
   bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank
-  std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
+  std::vector<int> algoSplit;
+  std::vector<int> algoSendRun;    // per algorithm: longest run of send chunks before a receive (any tb)      // workgroups per XML thread block, per algorithm (same on all ranks)
   int maxSplit = 1;                // sub-connections per (channel, peer)
   int coResident = 1;              // ranks of this communicator on this rank's GPU
 

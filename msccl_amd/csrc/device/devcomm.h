@@ -19,7 +19,15 @@
 
 namespace msccl {
 
-constexpr int kFifoSteps = 8;          // NCCL_STEPS
+constexpr int kFifoSteps = 8;          // NCCL_STEPS: Simple FIFO slots per sub-connection
+// LL / LL128 FIFO slots per sub-connection (the same 8 as the reference's NCCL_STEPS).
+// Calls may be merged here (full iterations, a transfer's chunks), which the reference never
+// does.  What a merged call must not break is that a thread block's sends issued before its next
+// receive fit its FIFO (both ends of a pair may send first).  The host bounds every run of
+// consecutive sends of a schedule to kMaxRunSlots slots per sub-connection: half the FIFO, so
+// one launch iteration's run can also sit behind the previous one unconsumed.
+constexpr int kLLFifoSlots = kFifoSteps;
+constexpr int kMaxRunSlots = 4;
 constexpr int kMaxLaunchRanks = 16;    // ranks fused into one launch (same device, same group)
 constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag padding)
 constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
@@ -63,7 +71,7 @@ struct alignas(16) DevTbHeader {
 static_assert(sizeof(DevTbHeader) == 16, "DevTbHeader must be 16 bytes");
 
 struct DevSendConn {
-  LLLine* ll;                  // receiver's LL FIFO (peer memory)  [kFifoSteps][llSlotLines]
+  LLLine* ll;                  // receiver's LL FIFO (peer memory)  [kLLFifoSlots][llSlotLines]
   char* simple;                 // receiver's Simple FIFO (peer memory) [kFifoSteps][simpleSlotBytes]
   uint64_t* remoteTail;         // receiver's tail word (peer memory)
   uint64_t* head;               // my head word, written by the receiver
@@ -132,6 +140,7 @@ struct RankWork {
   uint8_t maxAllowedCount;
   uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
   uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
+  int64_t maxOpElems;           // largest run of sends before a receive (elements, all sub-connections)
   // ring fallback (kRingNone for MSCCL schedules): the program's offsets are chunk / rank indices
   // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)
   uint8_t ringColl;

@@ -116,15 +116,16 @@ struct Interp {
     return false;
   }
 
-  // Send credit: the receiver has freed slot `sendStep` once head + kFifoSteps > sendStep.  The
+  // Send credit: the receiver has freed slot `sendStep` once head + SLOTS > sendStep.  The
   // last head seen is kept (and persisted in the connection), so most steps need no poll of the
   // remote word, whose round trip is the largest part of a small message's latency.
+  template <int SLOTS>
   __device__ __forceinline__ void waitSendCredit() {
-    if (headSeen + kFifoSteps >= sendStep + 1) return;
+    if (headSeen + SLOTS >= sendStep + 1) return;
     if (tid == 0) {
       uint32_t spins = 0;
       uint64_t h;
-      while ((h = atomicLoadSys(sc->head)) + kFifoSteps < sendStep + 1) {
+      while ((h = atomicLoadSys(sc->head)) + SLOTS < sendStep + 1) {
         if (spinAbort(spins)) break;
       }
       sh->seen[0] = h;
@@ -213,15 +214,15 @@ struct Interp {
     int s0 = 0;
     do {
       const int s1 = s.npk - s0 < slotPacks ? s.npk : s0 + slotPacks;
-      if (SEND) waitSendCredit();
+      if (SEND) waitSendCredit<kLLFifoSlots>();
       LLLine* rslot = nullptr;
       uint32_t rflag = 0, sflag = 0;
       if (RECV) {
-        rslot = rc->ll + (recvStep % kFifoSteps) * (uint64_t)rc->llSlotLines;
+        rslot = rc->ll + (recvStep % kLLFifoSlots) * (uint64_t)rc->llSlotLines;
         rflag = (uint32_t)(recvStep + 1);
       }
       if (SEND) {
-        frs = makeRsrc(sc->ll + (sendStep % kFifoSteps) * (uint64_t)sc->llSlotLines);
+        frs = makeRsrc(sc->ll + (sendStep % kLLFifoSlots) * (uint64_t)sc->llSlotLines);
         sflag = (uint32_t)(sendStep + 1);
       }
       if constexpr (kL16) {
@@ -413,7 +414,7 @@ struct Interp {
     for (int s0 = 0; s0 < s.npk; s0 += slicePacks) {
       const int s1 = s.npk - s0 < slicePacks ? s.npk : s0 + slicePacks;
       if (RECV) waitRecvTail();
-      if (SEND) waitSendCredit();
+      if (SEND) waitSendCredit<kFifoSteps>();
       __syncthreads();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
@@ -689,7 +690,8 @@ struct Interp {
         // (enqueue.cc:700-711); these primitives cut calls into FIFO steps themselves, so when the
         // iteration covers whole chunks (consecutive chunks are contiguous) a transfer's chunks
         // move as one call.  Not for `re`: its per-element path depends on the call's size.
-        const int macT = (t.type != tRe && !ringColl && nelem == sizePer) ? t.count : mac;
+        const int macT = (t.type != tRe && !ringColl && nelem == sizePer &&
+                          (t.type != tSend || (int64_t)nelem * t.count <= w.maxOpElems)) ? t.count : mac;
         for (int c = 0; c < t.count; c += macT) {
           int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
           int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;

@@ -159,10 +159,22 @@ RankWork makeWork(Planned& p) {
   // the device, so any merge fits; by default every full iteration runs in one op (fewest
   // dependency rounds).  maxAllowedCount is 1 whenever there is more than one iteration, so one
   // op never exceeds one chunk.
+  // Merged calls keep every run of sends before a receive within kMaxRunSlots FIFO slots per
+  // sub-connection (devcomm.h); a workgroup moves 1/split of a call.  sendRun = the schedule's
+  // longest such run in chunks (algoSendRun).
+  int64_t slotPacks;
+  if (p.plan.proto == kProtoSimple) slotPacks = comm->simpleSlotBytes / 16;
+  else if (p.plan.proto == kProtoLL128) slotPacks = (int64_t)(comm->llSlotLines / 256) * 64 * 3;
+  else slotPacks = comm->llSlotLines / 2;
+  w.maxOpElems = (int64_t)kMaxRunSlots * slotPacks * pe * split;
+  const int64_t sendRun = std::max(1, comm->algoSendRun.empty() ? 1 : comm->algoSendRun[p.plan.algoIndex]);
   int merge = 1;
   if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {
     const int64_t envMerge = envInt("MSCCL_AMD_MERGE", 0);
-    merge = envMerge > 0 ? (int)envMerge : 64;  // every full iteration in one op: fewest phases (bench: 32 MiB LL 348 -> 390 GB/s)
+    // as many full iterations per call as the bound allows: fewest dependency rounds
+    // (C2 32 MiB LL: 348 GB/s with `split` iterations per call, 405 with all 16)
+    const int64_t fit = std::max<int64_t>(1, w.maxOpElems / (std::max<int64_t>(1, p.plan.chunkSize) * sendRun));
+    merge = (int)std::min<int64_t>(envMerge > 0 ? envMerge : fit, fit);  // MSCCL_AMD_MERGE only lowers it
     merge = std::max(1, std::min(merge, 64));
   }
   w.merge = (uint8_t)merge;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
 #include <map>
 
 #include "comm.h"
@@ -80,7 +81,7 @@ ncclResult_t transportPlan(ncclComm* comm) {
   for (auto& kv : recvs) { comm->recvKeys.push_back(kv.first); comm->recvProtoMask.push_back(kv.second); }
 
   const int S = comm->maxSplit;
-  const int64_t llBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->llSlotLines * 16, kFifoAlign);
+  const int64_t llBytes = (int64_t)alignUp((size_t)kLLFifoSlots * comm->llSlotLines * 16, kFifoAlign);
   const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
   comm->table.assign((size_t)kTableChannels * n, PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
   // ring keys have a single sub-connection: stride 0 makes every sub alias sub 0
@@ -270,8 +271,25 @@ ncclResult_t ringUpload(ncclComm* comm) {
 
 // Pack every algorithm's per-tb programs and upload them (replaces the 29 MB
 // mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
+// Longest run of chunks a thread block sends before it next receives (merge bound, devcomm.h).
+static int sendRunOf(const Algorithm& a) {
+  int best = 0;
+  for (int b = 0; b < a.nBlocks; b++) {
+    int run = 0;
+    for (const Transfer& t : a.tbs[b].transfers) {
+      if (t.type == kSend) run += t.count;
+      else if (t.type == kRecv || t.type == kRecvCopySend || t.type == kRecvReduceSend ||
+               t.type == kRecvReduceCopy || t.type == kRecvReduceCopySend) run = 0;
+      best = std::max(best, run);
+    }
+  }
+  return best;
+}
+
 ncclResult_t algoUpload(ncclComm* comm) {
   comm->devAlgos.clear();
+  comm->algoSendRun.clear();
+  for (auto& a : comm->algos) comm->algoSendRun.push_back(sendRunOf(a));
   for (auto& a : comm->algos) {
     DevAlgoHost d;
     d.nBlocks = a.nBlocks;

@@ -188,3 +188,15 @@ def test_ll_and_ll128_share_a_fifo(tmp_path):
     finally:
         for c in comms:
             c.destroy()
+
+
+@pytest.mark.parametrize("proto,n,count,dt", [
+    ("Simple", 2, 2 * (1 << 22) + 2 * 512, 9),   # 4 M bf16 per chunk: 16 Simple iterations
+    ("LL", 2, 2 * (1 << 20), 7),                 # 1 M fp32 per chunk: 128 LL iterations
+])
+def test_large_calls_respect_fifo_depth(proto, n, count, dt, monkeypatch):
+    """Both ranks of a ring send before they receive.  Merged calls (iterations, a transfer's
+    chunks) stay within kMaxOpSlots FIFO slots per sub-connection, so one workgroup per thread
+    block (no split) must not deadlock on a call larger than its FIFO."""
+    monkeypatch.setenv("MSCCL_AMD_SPLIT", "1")
+    check(xmlgen.allreduce_ring(n, 1, proto), n, L.ALLREDUCE, count, dt, mode="exact")
