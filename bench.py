@@ -274,6 +274,11 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
 
 def main():
     a = parse()
+    # Only the result line goes to stdout: libraries that print there (gloo's connection report,
+    # HIP runtime messages) are sent to stderr at the file-descriptor level.
+    sys.stdout.flush()
+    result_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -429,7 +434,8 @@ def main():
     if extras:
         out["configs"] = extras
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(result_fd, (json.dumps(out) + "\n").encode())
     for c in comms:
         c.destroy()
     if multi:
