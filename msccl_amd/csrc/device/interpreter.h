@@ -257,6 +257,157 @@ struct Interp {
     } while (s0 < s.npk);
   }
 
+  // ---------------------------------------------------------------- LL128, 1/2/4-byte types
+  // One FIFO line per lane.  A unit of 3 packs (48 B) travels as 4 lines {12 B payload, 4-B
+  // flag} (the same line contents as l16Step); lane (unit u, line j) carries payload bytes
+  // [12j, 12j+12) of unit u in line 4u + j of the slot, so a wave's source loads (dwordx3), line
+  // stores and line polls are each one contiguous 768 B / 1 KiB.  Units never straddle two
+  // chunks of a split workgroup.  (8-byte elements straddle lanes: they take l16Step.)
+  template <int RECV, int SEND, int SRC, int DST>
+  __device__ void l16Op(const T* src, T* dst, const Shape s) {
+    constexpr int UL = 4;  // lines per lane per pass (8 spills: 128 VGPRs)
+    const int slotLines = uni(SEND ? sc->llSlotLines : rc->llSlotLines);
+    const int unitsPerSlot = slotLines / 4;
+    const bool contig = s.Lq == s.Q;  // the call's packs are one contiguous range
+    const int upc = contig ? 1 : (s.Lq + 2) / 3;  // units per chunk segment (split)
+    const int nUnits = contig ? (s.npk + 2) / 3 : (s.Lq > 0 ? (s.npk / s.Lq) * upc : 0);
+    const int64_t nbytes = (int64_t)s.n * TS;
+    __amdgpu_buffer_rsrc_t srs, drs, frs;
+    if (SRC) srs = makeRsrc(src);
+    if (DST) drs = makeRsrc(dst);
+    const bool vec = (!SRC || aligned16(src)) && (!DST || aligned16(dst));
+    int u0 = 0;
+    do {
+      const int u1 = nUnits - u0 < unitsPerSlot ? nUnits : u0 + unitsPerSlot;
+      if (SEND) waitSendCredit<kLLFifoSlots>();
+      LLLine* rslot = nullptr;
+      uint32_t rflag = 0, sflag = 0;
+      if (RECV) {
+        rslot = rc->ll + (recvStep % kLLFifoSlots) * (uint64_t)rc->llSlotLines;
+        rflag = (uint32_t)(recvStep + 1);
+      }
+      if (SEND) {
+        frs = makeRsrc(sc->ll + (sendStep % kLLFifoSlots) * (uint64_t)sc->llSlotLines);
+        sflag = (uint32_t)(sendStep + 1);
+      }
+      const int nLines = (u1 - u0) * 4;
+      for (int base = tid; base < nLines; base += kNT * UL) {
+        bool has[UL];
+        uint32_t sb[UL];
+        int vb[UL];
+        u32x3 v[UL];
+#pragma unroll
+        for (int k = 0; k < UL; k++) {
+          const int L = base + k * kNT;
+          const int u = u0 + (L >> 2), j = L & 3;
+          int bp, nv;
+          if (contig) {
+            bp = 3 * u;
+            nv = s.npk - bp < 3 ? s.npk - bp : 3;
+          } else {
+            const int c = u / upc, uu = u - c * upc;
+            bp = c * s.Q + s.q0 + 3 * uu;
+            nv = s.Lq - 3 * uu < 3 ? s.Lq - 3 * uu : 3;
+          }
+          has[k] = L < nLines && 3 * j < 4 * nv;  // this line carries payload
+          sb[k] = (uint32_t)(bp * 16 + 12 * j);
+          int64_t lim = (int64_t)16 * nv - 12 * j;
+          const int64_t left = nbytes - (int64_t)sb[k];
+          lim = left < lim ? left : lim;
+          vb[k] = has[k] ? (int)(lim < 0 ? 0 : (lim > 12 ? 12 : lim)) : 0;
+          v[k] = (u32x3){0, 0, 0};
+        }
+        if (SRC) {
+#pragma unroll
+          for (int k = 0; k < UL; k++) {
+            if (vb[k] == 12 && vec) v[k] = ld12<kAuxLocal>(srs, sb[k]);
+            else if (vb[k] > 0) v[k] = loadBytes12(srs, sb[k], vb[k]);
+          }
+        }
+        if (RECV) {
+          const void* la[UL];
+          u32x4 ln[UL];
+#pragma unroll
+          for (int k = 0; k < UL; k++) la[k] = rslot + (has[k] ? base + k * kNT : 0);
+          ldLines4(la, ln);
+#pragma unroll
+          for (int k = 0; k < UL; k++) {
+            uint32_t spins = 0;
+            while (has[k] && ln[k].w != rflag) {
+              if (spinAbort(spins)) break;
+              ldLine1(la[k], ln[k]);
+            }
+            const u32x4 peer = {ln[k].x, ln[k].y, ln[k].z, 0};
+            if (SRC) {
+              const u32x4 r = F::pack(peer, (u32x4){v[k].x, v[k].y, v[k].z, 0});
+              v[k] = (u32x3){r.x, r.y, r.z};
+            } else {
+              v[k] = (u32x3){peer.x, peer.y, peer.z};
+            }
+          }
+        }
+        if (SEND) {
+#pragma unroll
+          for (int k = 0; k < UL; k++)
+            if (has[k]) st16<kAuxFifo>(frs, (uint32_t)(base + k * kNT) * 16, (u32x4){v[k].x, v[k].y, v[k].z, sflag});
+        }
+        if (DST) {
+#pragma unroll
+          for (int k = 0; k < UL; k++) {
+            if (vb[k] == 12 && vec) st12<kAuxLocal>(drs, sb[k], v[k]);
+            else if (vb[k] > 0) storeBytes12(drs, sb[k], vb[k], v[k]);
+          }
+        }
+      }
+      if (SEND) {
+        if ((sendStep & kLLCleanMask) == kLLCleanMask) {
+          // LL cleanup (prims_ll.h:90-97): stamp every line of the slot that carries no payload
+          for (int l = tid; l < slotLines; l += kNT) {
+            const int u = u0 + (l >> 2), j = l & 3;
+            bool used = false;
+            if (l < nLines) {
+              int nv;
+              if (contig) nv = s.npk - 3 * u < 3 ? s.npk - 3 * u : 3;
+              else {
+                const int uu = u - (u / upc) * upc;
+                nv = s.Lq - 3 * uu < 3 ? s.Lq - 3 * uu : 3;
+              }
+              used = 3 * j < 4 * nv;
+            }
+            if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
+          }
+        }
+        sendStep++;
+      }
+      if (RECV) {
+        recvStep++;
+        __syncthreads();
+        if (tid == 0) atomicStoreSys(rc->remoteHead, recvStep);
+      }
+      u0 = u1;
+    } while (u0 < nUnits);
+  }
+
+  // up to 12 bytes (whole elements) of a line's payload, zero-filled
+  __device__ __forceinline__ u32x3 loadBytes12(__amdgpu_buffer_rsrc_t r, uint32_t off, int nb) {
+    T e[12 / TS];
+#pragma unroll
+    for (int i = 0; i < 12 / TS; i++) {
+      if (i * TS < nb) e[i] = ldElem<T>(r, off + i * TS);
+      else __builtin_memset(&e[i], 0, TS);
+    }
+    u32x3 o;
+    __builtin_memcpy(&o, e, 12);
+    return o;
+  }
+  __device__ __forceinline__ void storeBytes12(__amdgpu_buffer_rsrc_t r, uint32_t off, int nb, u32x3 x) {
+    T e[12 / TS];
+    __builtin_memcpy(e, &x, 12);
+#pragma unroll
+    for (int i = 0; i < 12 / TS; i++)
+      if (i * TS < nb) stElem<T>(r, off + i * TS, e[i]);
+  }
+
   // one LL step: packs [s0, s1) of the call, U packs per lane per pass with all their loads and
   // line polls in flight together
   template <int RECV, int SEND, int SRC, int DST>
@@ -469,7 +620,8 @@ struct Interp {
   template <int RECV, int SEND, int SRC, int DST>
   __device__ __forceinline__ void op(const T* src, T* dst, const Shape s) {
     if constexpr (PROTO == pSimple) simpleOp<RECV, SEND, SRC, DST>(src, dst, s);
-    else llOp<RECV, SEND, SRC, DST>(src, dst, s);  // LL and LL128
+    else if constexpr (PROTO == pLL128 && TS <= 4) l16Op<RECV, SEND, SRC, DST>(src, dst, s);
+    else llOp<RECV, SEND, SRC, DST>(src, dst, s);  // LL, and LL128 of 8-byte types
   }
 
   // ---------------------------------------------------------------- local ops

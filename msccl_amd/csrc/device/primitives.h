@@ -47,6 +47,16 @@ __device__ __forceinline__ uint64_t uni(uint64_t x) {
          __builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+template <int AUX>
+__device__ __forceinline__ u32x3 ld12(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void st12(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x3 v) {
+  __builtin_amdgcn_raw_buffer_store_b96(v, r, off, 0, AUX);
+}
+
 template <int AUX>
 __device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
@@ -97,6 +107,18 @@ __device__ __forceinline__ void ldLines2(const void* a, const void* b, u32x4& x,
       "s_waitcnt vmcnt(0)"
       : "=&v"(x), "=&v"(y)
       : "v"(a), "v"(b)
+      : "memory");
+}
+// Four FIFO lines in flight, one wait.
+__device__ __forceinline__ void ldLines4(const void* const* p, u32x4* x) {
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc0 sc1\n\t"
+      "global_load_dwordx4 %1, %5, off sc0 sc1\n\t"
+      "global_load_dwordx4 %2, %6, off sc0 sc1\n\t"
+      "global_load_dwordx4 %3, %7, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3])
       : "memory");
 }
 // Eight FIFO lines (four packs) in flight, one wait.
