@@ -37,6 +37,16 @@ CASES = [
      False, "uniform"),
     ("ag8_ll_f32", lambda: xmlgen.allgather_allpairs(8, 2, "LL"), 8, L.ALLGATHER, 512, 7, 0, False, "uniform"),
     ("ap2_ll_i32_exact", lambda: xmlgen.allreduce_allpairs(2, 2, "LL"), 2, L.ALLREDUCE, 1024, 2, 0, True, "exact"),
+    ("ap4_ll128_f16", lambda: xmlgen.allreduce_allpairs(4, 2, "LL128"), 4, L.ALLREDUCE, 32 * 1001, 6, 0, True,
+     "uniform"),
+]
+
+# Ring fallback (no schedule matches, oracle/ring.py): name, nranks, coll, count, dtype, op, inplace
+RING_CASES = [
+    ("fb3_ring_ar_f32", 3, L.ALLREDUCE, 5003, 7, 0, True),
+    ("fb4_ring_rs_bf16", 4, L.REDUCE_SCATTER, 3001, 9, 0, False),
+    ("fb2_ring_ag_f16", 2, L.ALLGATHER, 777, 6, 0, False),
+    ("fb8_ring_ar_f16_max", 8, L.ALLREDUCE, 100003, 6, 2, False),
 ]
 
 
@@ -76,7 +86,26 @@ def run_case(xml, n, coll, count, dt, op, inplace, mode, seed=7):
     return ins, [np.array(r) for r in res]
 
 
+def run_ring_case(n, coll, count, dt, op, inplace, seed=7):
+    from oracle import ring as R
+    in_n = count * n if coll == L.REDUCE_SCATTER else count
+    ins = gen_inputs(n, in_n, dt, seed, "uniform")
+    if coll == L.ALLGATHER:
+        outs = [np.zeros(count * n, ins[0].dtype) for _ in range(n)]
+    elif inplace:
+        outs = [None] * n
+    else:
+        outs = [np.zeros(count, ins[0].dtype) for _ in range(n)]
+    res, _ = R.run(coll, count, dt, op, [x.copy() for x in ins], outs, inplace)
+    return ins, [np.array(r) for r in res]
+
+
 def main():
+    for (name, n, coll, count, dt, op, inplace) in RING_CASES:
+        ins, outs = run_ring_case(n, coll, count, dt, op, inplace)
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), inputs=np.stack(ins), outputs=np.stack(outs),
+                            meta=np.array([n, coll, count, dt, op, int(inplace)], dtype=np.int64))
+        print("wrote", name)
     for (name, xf, n, coll, count, dt, op, inplace, mode) in CASES:
         xml = xf()
         ins, outs = run_case(xml, n, coll, count, dt, op, inplace, mode)

@@ -110,7 +110,7 @@ def test_rccl_ring16_ll(rccl_xmls):
     check(text, 16, L.ALLREDUCE, 384 * 4, 7)
 
 
-@pytest.mark.parametrize("name", ["ap2_ll_f32", "ap4_ll_bf16", "ring8_simple_bf16", "rs8_simple_f32",
+@pytest.mark.parametrize("name", ["ap2_ll_f32", "ap4_ll_bf16", "ring8_simple_bf16", "rs8_simple_f32", "ap4_ll128_f16",
                                   "ag8_ll_f32", "ap8_ll_f16_rccl32tb", "ap2_ll_i32_exact"])
 def test_golden_vectors_on_gpu(name):
     from tests.golden import make_golden as G

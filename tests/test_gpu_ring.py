@@ -59,3 +59,14 @@ def test_ring_channels_forced(monkeypatch):
     monkeypatch.setenv("MSCCL_AMD_RING_CHANNELS", "3")
     rp = check(4, L.ALLREDUCE, 654321, 9)
     assert rp["channels"] == 3
+
+
+@pytest.mark.parametrize("name", ["fb3_ring_ar_f32", "fb4_ring_rs_bf16", "fb2_ring_ag_f16", "fb8_ring_ar_f16_max"])
+def test_ring_golden_vectors_on_gpu(name):
+    from tests.golden import make_golden as G
+    from tests.gpu_harness import run_ring_fallback
+    _, n, coll, count, dt, op, inplace = [c for c in G.RING_CASES if c[0] == name][0]
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
+    gpu, _, _ = run_ring_fallback(n, coll, count, dt, op, inplace, seed=7)
+    for r in range(n):
+        assert np.array_equal(gpu[r].view(np.uint8), z["outputs"][r].view(np.uint8)), r

@@ -76,3 +76,16 @@ def test_ring_plan_env(tmp_path, monkeypatch):
     # Avg has no ring in this build (PreMulSum/SumPostDiv are not provided)
     monkeypatch.delenv("MSCCL_AMD_RING_FALLBACK")
     assert "ring" not in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 4, True)
+
+
+from tests.golden import make_golden as G  # noqa: E402
+
+
+@pytest.mark.parametrize("case", G.RING_CASES, ids=[c[0] for c in G.RING_CASES])
+def test_ring_golden(case):
+    import os
+    name, n, coll, count, dt, op, inplace = case
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
+    ins, outs = G.run_ring_case(n, coll, count, dt, op, inplace)
+    assert np.array_equal(np.stack(ins), z["inputs"])
+    assert np.array_equal(np.stack(outs).view(np.uint8), z["outputs"].view(np.uint8))
