@@ -193,7 +193,8 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
     // a peer is remote (xGMI) unless it runs on the same GPU: same host and PCI bus id
     std::vector<int> peerRemote(n, 0);
     for (int r = 0; r < n; r++)
-      peerRemote[r] = strcmp(recs[r].host, srec.host) != 0 || strcmp(recs[r].bus, srec.bus) != 0;
+      peerRemote[r] = strcmp(recs[r].host, srec.host) != 0 || strcmp(recs[r].bus, srec.bus) != 0 ||
+                      envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;  // test knob: xGMI ordering on one GPU
     for (int r = 0; r < n; r++) {
       tables[r].resize(comm->table.size());
       memcpy(tables[r].data(), tall.data() + (size_t)r * tbytes, tbytes);
@@ -352,7 +353,8 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
         }
       }
       std::vector<int> remote(ndev);
-      for (int j = 0; j < ndev; j++) remote[j] = cs[j]->cudaDev != cs[i]->cudaDev;
+      for (int j = 0; j < ndev; j++)
+        remote[j] = cs[j]->cudaDev != cs[i]->cudaDev || envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;
       cs[i]->peerArena = bases;
       cs[i]->peerArenaIpc.assign(ndev, false);
       if (res == ncclSuccess) res = transportConnect(cs[i], tables, bases, remote);

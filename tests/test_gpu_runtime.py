@@ -301,3 +301,13 @@ def test_device_trace_records_every_transfer(tmp_path, monkeypatch):
     finally:
         for c in comms:
             c.destroy()
+
+
+@pytest.mark.parametrize("proto", ["Simple", "LL", "LL128"])
+def test_remote_ordering_path(proto, monkeypatch):
+    """MSCCL_AMD_FORCE_REMOTE=1 treats every peer as another GPU (system-scope release before a
+    Simple tail post, as for xGMI peers): same values, bit-exact."""
+    from tests.test_gpu_parity import check
+    monkeypatch.setenv("MSCCL_AMD_FORCE_REMOTE", "1")
+    check(xmlgen.allreduce_allpairs(4, 2, proto), 4, L.ALLREDUCE, 32 * 5001, 7)
+    check(xmlgen.allreduce_ring(4, 2, proto), 4, L.ALLREDUCE, 8 * 7777, 9)
