@@ -425,6 +425,10 @@ def main():
                    "launch": "hipgraph" if a.graph else "eager",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
+        # `value` is the metric as BASELINE.json and nccl-tests define it (bus bandwidth seen by
+        # each rank); the whole job moves n_ranks times that
+        "aggregate": {"ranks": n, "busbw_sum_gbs": round(head["busbw"] * n, 3),
+                      "algbw_sum_gbs": round(head["bytes"] / (head["ms"] / 1e3) / 1e9 * n, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
         "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw")} for r in results],
