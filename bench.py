@@ -188,6 +188,10 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, 4, "Simple", False, 0, 1 << 40, name="c5_rs"),
                 "ag": xmlgen.allgather_allpairs(n, 4, "Simple", False, 0, 1 << 40, name="c5_ag")}
         dt, S = M.FLOAT32, 64 << 20
+    elif cfg == "FB":
+        # ring fallback (enqueue.cc:461-476): 32 MiB + one element matches no all-pairs schedule
+        xmls = {"ap": xmlgen.allreduce_allpairs(n, 1, "LL", True, 0, 1 << 40, name="fb_ap")}
+        dt, S = M.FLOAT32, (32 << 20) + 4
     else:
         raise ValueError(cfg)
     paths = []
@@ -207,9 +211,9 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
     stream = torch.cuda.Stream(dev)
     nloc = len(comms)
     try:
-        if cfg == "C4":
+        if cfg in ("C4", "FB"):
             cnt = S // ts
-            bufs = [torch.zeros(S // 2, dtype=torch.int16, device=dev) for _ in range(nloc)]
+            bufs = [torch.zeros((S + 1) // 2, dtype=torch.int16, device=dev) for _ in range(nloc)]
 
             def step():
                 with M.group():
@@ -264,8 +268,9 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         res["bytes"] = S
         res["dtype"] = {M.BFLOAT16: "bf16", M.FLOAT32: "f32"}[dt]
         res["ranks"] = n
-        res["schedule"] = "allreduce_ring x%d Simple" % (8 if n >= 8 else max(1, n)) if cfg == "C4" else \
-            "reduce_scatter_allpairs + allgather_allpairs x4 Simple"
+        res["schedule"] = {"C4": "allreduce_ring x%d Simple" % (8 if n >= 8 else max(1, n)),
+                           "C5": "reduce_scatter_allpairs + allgather_allpairs x4 Simple",
+                           "FB": "ring fallback (no schedule matches)"}[cfg]
         return res
     finally:
         for c in comms:

@@ -26,7 +26,7 @@ constexpr int kRefWarp = 32;                // reference WARP_SIZE (used only in
 constexpr int kMaxIter = 65536;             // MSCCL_MAX_ITER (msccl_interpreter.h:10)
 // Ring fallback (enqueue.cc:461-476): channels kRingChanBase.. of the connection table carry
 // one ring (send to rank+1, receive from rank-1) each; XML channels are 0..32.
-constexpr int kRingChannels = 8;
+constexpr int kRingChannels = 32;  // as many as the reference's MAXCHANNELS
 constexpr int kRingChanBase = 40;
 constexpr int kTableChannels = kRingChanBase + kRingChannels;
 

@@ -16,7 +16,7 @@ Where the reference consults its topology search and tuning model (graph/search.
 tuning.cc:77-309, enqueue.cc:486-515), this build decides as follows; ring_params() states it and
 msccl_amd/csrc/plan.cc (makeRingPlan) mirrors it:
   * the ring order is the rank order: ringRanks of rank r = [r, r+1, ..., r-1] (mod n);
-  * channels = min(8, max(1, nBytes >> 18)) (MSCCL_AMD_RING_CHANNELS forces it);
+  * channels = min(32, max(1, nBytes >> 18)) (MSCCL_AMD_RING_CHANNELS forces it);
   * LL when nBytes <= 512 KiB, else Simple (NCCL_PROTO masks them; LL128 is not used here);
   * nThreads is not reduced for small messages (the reference halves it below its thresholds).
 """
@@ -31,7 +31,7 @@ from . import loader as L
 from . import numerics as N
 from . import plan as P
 
-RING_MAX_CHANNELS = 8
+RING_MAX_CHANNELS = 32
 RING_LL_MAX_BYTES = 512 << 10
 REF_WARP = 32
 

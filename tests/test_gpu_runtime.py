@@ -141,7 +141,7 @@ def test_no_match_falls_back_to_ring(tmp_path):
             for b in o:
                 assert torch.equal(b.cpu(), x[0] + x[1]), (count, inplace)
         assert all(c.async_error() == 0 for c in comms)
-        assert comms[0].info()["sendConns"] == 4 + 8   # 4 all-pairs channels + 8 ring channels
+        assert comms[0].info()["sendConns"] == 4 + 32   # 4 all-pairs channels + 32 ring channels
     finally:
         for c in comms:
             c.destroy()
