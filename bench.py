@@ -59,7 +59,7 @@ def parse():
 
 def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int):
     """Algorithmic HBM bytes and wire bytes of one launch for one rank (whole schedule)."""
-    f = 2 if proto in (0, 1) else 1  # LL: a 16-B line carries 8 B of data
+    f = {0: 2.0, 1: 4.0 / 3.0}.get(proto, 1.0)  # LL: 8 B data per 16-B line; CDNA4 LL128: 12 B
     hbm = wire = 0
     for tb in algo["tbs"]:
         for t in tb["transfers"]:
@@ -81,7 +81,7 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int):
                 hbm += 2 * b
             elif typ == 7:    # re
                 hbm += (nred + 1) * b + b
-    return hbm, wire
+    return int(round(hbm)), int(round(wire))
 
 
 def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
