@@ -128,6 +128,14 @@ struct RankWork {
   void* recvbuff;
   void* scratch;
   DevComm* comm;
+  // copies of the DevComm fields every workgroup needs at start (kernel arguments: no
+  // dependent global load before the first connection / epoch load)
+  DevSendConn* send;
+  DevRecvConn* recv;
+  uint64_t* flags;
+  uint64_t* epochs;
+  int32_t maxSplit;
+  int32_t pad0;
   const DevTbHeader* tbs;
   const char* blob;
   int64_t sizePerChunk;         // sizePerMscclChunk = count*sizeMultiplier/nchunksPerLoop (elements)
@@ -163,3 +171,5 @@ typedef int (*LaunchFn)(const LaunchArgs& args, int gridBlocks, void* stream);
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
 
 }  // namespace msccl
+
+static_assert(sizeof(msccl::LaunchArgs) <= 4096, "kernel argument block must stay within 4 KiB");

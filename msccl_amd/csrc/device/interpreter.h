@@ -705,7 +705,7 @@ struct Interp {
     refNthreads = w.refNthreads;
     t0 = __builtin_amdgcn_s_memrealtime();
     const int split = w.split;
-    const int maxSplit = comm->maxSplit;
+    const int maxSplit = w.maxSplit;
     const int slot = bid * maxSplit + sub;  // flag / epoch / trace slot of this workgroup
     DevTbHeader hd;
     {
@@ -722,8 +722,8 @@ struct Interp {
       sh->depStep[i] = gdep[hd.ndeps + i];
     }
     for (int i = tid; i < hd.nreds; i += kNT) sh->red[i] = gdep[2 * hd.ndeps + i];
-    scG = hd.sendConn >= 0 ? comm->send + (size_t)hd.sendConn * maxSplit + sub : nullptr;
-    rcG = hd.recvConn >= 0 ? comm->recv + (size_t)hd.recvConn * maxSplit + sub : nullptr;
+    scG = hd.sendConn >= 0 ? w.send + (size_t)hd.sendConn * maxSplit + sub : nullptr;
+    rcG = hd.recvConn >= 0 ? w.recv + (size_t)hd.recvConn * maxSplit + sub : nullptr;
     static_assert(sizeof(DevSendConn) % 4 == 0 && sizeof(DevRecvConn) % 4 == 0, "connection copy");
     constexpr int kSW = sizeof(DevSendConn) / 4, kRW = sizeof(DevRecvConn) / 4;
     if (scG && tid < kSW) ((uint32_t*)&sh->sconn)[tid] = ((const uint32_t*)scG)[tid];
@@ -736,7 +736,7 @@ struct Interp {
       sh->seen[0] = scG ? scG->headSeen : 0;
       sh->seen[1] = rcG ? rcG->tailSeen : 0;
       sh->aborted = 0;
-      sh->epoch = atomicLoadAgent(comm->epochs + slot);
+      sh->epoch = atomicLoadAgent(w.epochs + slot);
     }
     __syncthreads();
     sendStep = uni(sh->step[0]);
@@ -755,7 +755,7 @@ struct Interp {
     const int64_t chunkSize = w.chunkSize;
     const int mac = w.maxAllowedCount;
     const uint64_t workIndex = uni(sh->epoch);  // COMPUTE_FLAG's workIndex (msccl_interpreter.h:14-16)
-    uint64_t* flags = comm->flags;
+    uint64_t* flags = w.flags;
     bool stop = false;
 
     const int64_t merge = w.merge;
@@ -920,14 +920,14 @@ struct Interp {
         rcG->step = recvStep;
         rcG->tailSeen = tailSeen;
       }
-      atomicStoreAgent(comm->epochs + slot, workIndex + 1);
+      atomicStoreAgent(w.epochs + slot, workIndex + 1);
     }
     {
       // advance the epoch of every slot this launch does not run (DevComm::epochs): launch
       // workgroup g covers the unlaunched slots j with j % launched == g
       const int launched = w.nBlocks, nTb = launched / split, g = bid * split + sub;
       for (int j = g + tid * launched; j < kFlagSlots; j += kNT * launched)
-        if (j / maxSplit >= nTb || j % maxSplit >= split) atomicStoreAgent(comm->epochs + j, workIndex + 1);
+        if (j / maxSplit >= nTb || j % maxSplit >= split) atomicStoreAgent(w.epochs + j, workIndex + 1);
     }
     ev(kEvEnd, 0, 0);
     if (trace != nullptr && tid == 0) {

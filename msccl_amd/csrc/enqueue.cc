@@ -110,6 +110,11 @@ RankWork makeRingWork(Planned& p) {
   w.recvbuff = p.op.recvbuff;
   w.scratch = comm->scratch;
   w.comm = comm->dComm;
+  w.send = comm->dSend;
+  w.recv = comm->dRecv;
+  w.flags = comm->dFlags;
+  w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  w.maxSplit = comm->maxSplit;
   w.tbs = da.dTbs;
   w.blob = da.dBlob;
   w.chunkSize = p.plan.chunkSize;
@@ -137,6 +142,11 @@ RankWork makeWork(Planned& p) {
   w.recvbuff = p.op.recvbuff;
   w.scratch = comm->scratch;
   w.comm = comm->dComm;
+  w.send = comm->dSend;
+  w.recv = comm->dRecv;
+  w.flags = comm->dFlags;
+  w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  w.maxSplit = comm->maxSplit;
   w.tbs = da.dTbs;
   w.blob = da.dBlob;
   w.sizePerChunk = p.plan.sizePerChunk;
