@@ -319,6 +319,12 @@ def main():
         if multi:
             torch.distributed.barrier()
 
+    xgmi_cal = None
+    if multi:
+        # SURVEY 8(d) calibration: one-way peer copy cuda:0 -> cuda:1 (xGMI), 256 MiB, rank 0
+        if rank == 0 and torch.cuda.device_count() > 1 and os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") != "1":
+            xgmi_cal = calibrate_xgmi()
+        barrier()
     stream = torch.cuda.Stream(devs[0])
     stream.wait_stream(torch.cuda.current_stream(devs[0]))
     maxb = max(sizes)
@@ -396,7 +402,8 @@ def main():
     if multi:
         link = XGMI_LINK_GBS * (n - 1)
         roof["xgmi"] = {"busbw": head["busbw"], "peak": link, "frac": round(head["busbw"] / link, 4),
-                        "ll_ceiling": round(link * (0.5 if proto_id == 0 else 1.0), 1)}
+                        "ll_ceiling": round(link * {0: 0.5, 1: 0.75}.get(proto_id, 1.0), 1),
+                        "link_gbs_assumed": XGMI_LINK_GBS, "link_gbs_measured": xgmi_cal}
     workload = workload_desc(multi, n, a.proto, dtname)
     knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("MSCCL_AMD_") and k != "MSCCL_AMD_TIMEOUT_SEC"}
     cfg_key = {"workload": workload, "bytes_per_rank": head["bytes"], "instances_large": inst, "knobs": knobs}
@@ -415,8 +422,8 @@ def main():
         except Exception as e:  # noqa: BLE001  (reported in the JSON line, the headline stands)
             extras[cfg] = {"error": str(e)[:300]}
     cpu = None
-    if not a.no_cpu and rank == 0:
-        cpu = cpu_baseline(2 if not multi else n, maxb, dt if dt in (6, 7, 9) else 7, a.cpu_seconds)
+    if not a.no_cpu and rank == 0 and not multi:   # the host baseline is quoted at N=1 only
+        cpu = cpu_baseline(n, maxb, dt if dt in (6, 7, 9) else 7, a.cpu_seconds)
     out = {
         "metric": "AllReduce bus-BW GB/s (device-resident), 128B-32MB",
         "value": head["busbw"], "unit": "GB/s", "n_gpus": world if multi else 1, "steps": a.steps,
@@ -449,6 +456,28 @@ def main():
         c.destroy()
     if multi:
         torch.distributed.destroy_process_group()
+
+
+def calibrate_xgmi(nbytes: int = 256 << 20, reps: int = 5):
+    """One-way device-to-device copy GB/s between cuda:0 and cuda:1 (is 153 GB/s
+    per link one-way?).  Returns None when the copy fails."""
+    import torch
+    try:
+        src = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+        dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda:1")
+        dst.copy_(src)
+        torch.cuda.synchronize("cuda:0")
+        torch.cuda.synchronize("cuda:1")
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize("cuda:0")
+        torch.cuda.synchronize("cuda:1")
+        gbs = nbytes * reps / (time.perf_counter() - t0) / 1e9
+        del src, dst
+        return round(gbs, 2)
+    except Exception:  # noqa: BLE001  (reported as unmeasured)
+        return None
 
 
 def measure_e2e(comms, n, nbytes, dt, ts, stream, dev):
