@@ -181,12 +181,15 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
     import torch
     dev = torch.device("cuda", torch.cuda.current_device())
     if cfg == "C4":
-        chans = 8 if n >= 8 else max(1, n)
+        # 32 rings (the reference's MAXCHANNELS) over the xGMI-disjoint Hamiltonian cycles of
+        # xmlgen.allreduce_ring: 2 co-resident ranks, 256 MiB bf16: 180 GB/s with 2 rings, 645 with 32
+        chans = int(os.environ.get("MSCCL_AMD_BENCH_C4_CHANNELS", "0")) or 32
         xmls = {"ar": xmlgen.allreduce_ring(n, chans, "Simple", True, 0, 1 << 40, name="c4_ring")}
         dt, S = M.BFLOAT16, 256 << 20
     elif cfg == "C5":
-        xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, 4, "Simple", False, 0, 1 << 40, name="c5_rs"),
-                "ag": xmlgen.allgather_allpairs(n, 4, "Simple", False, 0, 1 << 40, name="c5_ag")}
+        c5i = int(os.environ.get("MSCCL_AMD_BENCH_C5_INSTANCES", "0")) or 16  # 2 ranks: RS 126 -> 243, AG 225 -> 373 GB/s vs 4
+        xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_rs"),
+                "ag": xmlgen.allgather_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_ag")}
         dt, S = M.FLOAT32, 64 << 20
     elif cfg == "FB":
         # ring fallback (enqueue.cc:461-476): 32 MiB + one element matches no all-pairs schedule
@@ -268,8 +271,8 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         res["bytes"] = S
         res["dtype"] = {M.BFLOAT16: "bf16", M.FLOAT32: "f32"}[dt]
         res["ranks"] = n
-        res["schedule"] = {"C4": "allreduce_ring x%d Simple" % (8 if n >= 8 else max(1, n)),
-                           "C5": "reduce_scatter_allpairs + allgather_allpairs x4 Simple",
+        res["schedule"] = {"C4": "allreduce_ring x%d Simple" % chans if cfg == "C4" else "",
+                           "C5": "reduce_scatter_allpairs + allgather_allpairs x%d Simple" % c5i if cfg == "C5" else "",
                            "FB": "ring fallback (no schedule matches)"}[cfg]
         return res
     finally:

@@ -1,10 +1,6 @@
 #!/bin/bash
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-probe() {
-  echo "== $*"
-  timeout -k 10 120 env "$@" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print([ (s['bytes'], s['busbw'], s['kernel_ms']) for s in d['sweep']])" || exit 1
-}
-B="python bench.py --no-cpu --quiet --steps 40 --warmup 10 --sizes 128,65536,1048576,8388608,33554432"
-probe X=1 $B
-probe X=1 $B
+for i in 4 8 16; do
+  MSCCL_AMD_BENCH_C5_INSTANCES=$i timeout -k 10 200 python bench.py --no-cpu --quiet --steps 10 --warmup 3 --sizes 1048576 --extras C4,C5 2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print($i, d['configs'])" || exit 1
+done
