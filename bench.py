@@ -85,23 +85,36 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int):
 
 
 def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
-    """The all-pairs schedule in size tiers, as a user registers several msccl-tools XMLs with
-    minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path)].  Few instances
-    keep small messages divisible and latency-light; 8 instances suit 2-8 MiB on one GPU; the
-    large tier uses inst_large.  At 8 ranks: 1 instance below 64 KiB, inst_large above."""
+    """All-pairs schedules in size tiers, as a user registers several msccl-tools XMLs with
+    minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
+    ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
+    for n = 2) serves sizes below 8 MiB and the two-phase all-pairs the rest; the large tier uses
+    inst_large.  At more ranks: two-phase all-pairs, 1 instance below 64 KiB, inst_large above."""
     if tiers_arg:
-        spec = [tuple(int(v) for v in t.split(":")) for t in tiers_arg.split(",")]
+        # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot
+        spec = []
+        for t in tiers_arg.split(","):
+            f = t.split(":")
+            spec.append((int(f[0]), int(f[1]), int(f[2])) + ((f[3],) if len(f) > 3 else ()))
     elif n <= 2:
-        spec = [(0, 4 << 10, 1), (4 << 10, 2 << 20, inst_large), (2 << 20, 8 << 20, 8),
+        # below 8 MiB the one-shot schedule (s, r, re: 3 transfers on the critical path instead
+        # of 7) wins: 128 B 18.4 -> 13.3 us, 2 MiB 23.2 -> 19.7 us; from 8 MiB on the two-phase
+        # all-pairs moves fewer HBM bytes (7.5 S vs 9 S per rank) and wins (DESIGN.md §4)
+        spec = [(0, 4 << 10, 1, "o"), (4 << 10, 2 << 20, 16, "o"), (2 << 20, 8 << 20, 8, "o"),
                 (8 << 20, (1 << 30) + 1, inst_large)]
     else:
         spec = [(0, 64 << 10, 1), (64 << 10, (1 << 30) + 1, inst_large)]
     tiers = []
-    for k, (lo, hi, inst) in enumerate(spec):
-        x = xmlgen.allreduce_allpairs(n, inst, proto, True, lo, hi, name="allpairs_t%d_i%d" % (k, inst))
-        pth = os.path.join(tmp, "bench_ap%d_%s_t%d_i%d_%d.xml" % (n, proto, k, inst, os.getpid()))
+    for k, t in enumerate(spec):
+        lo, hi, inst = t[:3]
+        kind = t[3] if len(t) > 3 else "a"
+        if kind == "o":
+            x = xmlgen.allreduce_oneshot(n, inst, proto, lo, hi, name="oneshot_t%d_i%d" % (k, inst))
+        else:
+            x = xmlgen.allreduce_allpairs(n, inst, proto, True, lo, hi, name="allpairs_t%d_i%d" % (k, inst))
+        pth = os.path.join(tmp, "bench_ap%d_%s_t%d_i%d_%s_%d.xml" % (n, proto, k, inst, kind, os.getpid()))
         open(pth, "w").write(x)
-        tiers.append((lo, hi, inst, pth))
+        tiers.append((lo, hi, inst, pth, kind))
     return tiers
 
 
@@ -345,7 +358,7 @@ def main():
     for nbytes in sizes:
         cnt = nbytes // ts
         tier = tier_of(tiers, nbytes)
-        ncpl = tier[2] * n * n
+        ncpl = tier[2] * (n * n if tier[4] == "a" else 1)
         if cnt % ncpl:
             continue
         for _ in range(a.warmup):
@@ -436,7 +449,7 @@ def main():
         "config": {"workload": workload,
                    "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
-                   "tiers": [[t[0], t[1], t[2]] for t in tiers],
+                   "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot"}[t[4]]] for t in tiers],
                    "launch": "hipgraph" if a.graph else "eager",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),

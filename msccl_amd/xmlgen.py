@@ -151,6 +151,45 @@ def allreduce_allpairs(n: int, instances: int = 1, proto: str = "LL", inplace: b
     return _emit(name, proto, I, ncpl, n, "allreduce", inplace, gpus, min_bytes, max_bytes, nthreads)
 
 
+def allreduce_oneshot(n: int, instances: int = 1, proto: str = "LL",
+                      min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
+                      nthreads: Optional[int] = None, name: str = "allreduce_oneshot") -> str:
+    """One-shot all-pairs AllReduce (in place): every rank sends its whole buffer to every peer's
+    scratch, then reduces the n-1 received copies into its own buffer.  Three transfers on the
+    critical path (s, r, re) instead of the two-phase schedule's seven, for latency-bound sizes.
+    Each rank folds its own data first (re: d (+) s_p), so for n == 2 and a commutative op both
+    ranks hold the same bits; for n > 2 ranks may differ in floating-point rounding."""
+    if n < 2:
+        raise ValueError("oneshot needs at least 2 ranks")
+    I = instances
+    gpus = {}
+    for r in range(n):
+        peers = [p for p in range(n) if p != r]
+        red = [_Tb(k, -1, -1, k) for k in range(I)]
+        ptb = {}
+        for pi, p in enumerate(peers):
+            for k in range(I):
+                tb = _Tb(I + pi * I + k, p, p, k)
+                tb.add("s", "i", k, "s", k * (n - 1) + _slot_of(r, p), 1)
+                tb.add("r", "i", k, "s", k * (n - 1) + pi, 1, hasdep=1)
+                ptb[(k, p)] = tb
+        for k in range(I):
+            tb = red[k]
+            others = [ptb[(k, p)].id for p in peers]
+            for dep in others[1:]:
+                tb.nop(dep, 1)
+            for pi, p in enumerate(peers):
+                if pi == 0:
+                    tb.add("re", "s", k * (n - 1) + pi, "i", k, 1, others[0], 1)
+                else:
+                    tb.add("re", "s", k * (n - 1) + pi, "i", k, 1)
+        tbs = red + [ptb[(k, p)] for p in peers for k in range(I)]
+        gpus[r] = (I, 0, I * (n - 1), tbs)
+    if max_bytes is None:
+        max_bytes = 1 << 62
+    return _emit(name, proto, I, I, n, "allreduce", True, gpus, min_bytes, max_bytes, nthreads)
+
+
 def _slot_of(r: int, p: int) -> int:
     """scratch slot of sender r on receiver p: peers of p in ascending order, p skipped."""
     return r if r < p else r - 1

@@ -44,6 +44,19 @@ def test_allpairs_allreduce(proto, dt, n, inst, count):
 
 
 @pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
+@pytest.mark.parametrize("n,inst,count,dt", [
+    (2, 1, 32, 7),              # 128 B fp32 (the C2 sweep's first point)
+    (2, 16, 16 * 4099, 7),      # odd chunk: element tails, per-element reduce path off
+    (2, 16, (1 << 20), 6),
+    (4, 2, 2 * 3001, 9),
+    (8, 1, 8 * 1000, 7),
+])
+def test_oneshot_allreduce(proto, n, inst, count, dt):
+    """xmlgen.allreduce_oneshot (the bench's latency tier) vs the oracle, bit-exact."""
+    check(xmlgen.allreduce_oneshot(n, inst, proto), n, L.ALLREDUCE, count, dt)
+
+
+@pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
 def test_allpairs_out_of_place(proto):
     check(xmlgen.allreduce_allpairs(8, 2, proto, inplace=False), 8, L.ALLREDUCE, 128 * 513, 7, inplace=False)
 

@@ -29,12 +29,23 @@ def run(xml, n, coll, count, dt, op=0, inplace=True, mode="exact", seed=1):
     (lambda: xmlgen.allreduce_allpairs(8, 4, "LL", inplace=False), 8, 256 * 5, 9, False),
     (lambda: xmlgen.allreduce_ring(8, 4, "Simple"), 8, 32 * 257, 7, True),
     (lambda: xmlgen.allreduce_ring(5, 3, "LL", inplace=False), 5, 15 * 64, 8, False),
+    (lambda: xmlgen.allreduce_oneshot(2, 1, "LL"), 2, 33, 7, True),
+    (lambda: xmlgen.allreduce_oneshot(2, 4, "Simple"), 2, 4 * 1000, 7, True),
+    (lambda: xmlgen.allreduce_oneshot(4, 2, "LL128"), 4, 2 * 300, 6, True),
 ])
 def test_allreduce_exact_sum(xml, n, count, dt, inplace):
     ins, outs = run(xml(), n, L.ALLREDUCE, count, dt, inplace=inplace)
     want = sum(N.to_float64(dt, x) for x in ins)
     for r in range(n):
         assert np.array_equal(N.to_float64(dt, outs[r]), want)
+
+
+def test_oneshot_two_ranks_bitwise_identical_across_ranks():
+    """n = 2 one-shot: each rank folds fn(own, peer); commutative ops give both ranks the same bits."""
+    ins, outs = run(xmlgen.allreduce_oneshot(2, 2, "LL"), 2, L.ALLREDUCE, 2 * 777, 7, mode="uniform")
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    want = N.apply(0, 7, ins[0], ins[1])  # fp32 a + b, RNE
+    assert np.array_equal(outs[0].view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
 
 
 def test_reduce_scatter_allgather_exact():
