@@ -88,7 +88,7 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
     """All-pairs schedules in size tiers, as a user registers several msccl-tools XMLs with
     minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
     ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
-    for n = 2) serves sizes below 8 MiB and the two-phase all-pairs the rest; the large tier uses
+    for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
     inst_large.  At more ranks: two-phase all-pairs, 1 instance below 64 KiB, inst_large above."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot
@@ -97,11 +97,10 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
             f = t.split(":")
             spec.append((int(f[0]), int(f[1]), int(f[2])) + ((f[3],) if len(f) > 3 else ()))
     elif n <= 2:
-        # below 8 MiB the one-shot schedule (s, r, re: 3 transfers on the critical path instead
-        # of 7) wins: 128 B 18.4 -> 13.3 us, 2 MiB 23.2 -> 19.7 us; from 8 MiB on the two-phase
+        # below 16 MiB the one-shot schedule (s, r, re: 3 transfers on the critical path instead
+        # of 7) wins: 128 B 18.4 -> 13.3 us, 4 MiB 27.3 -> 24.2 us; from 16 MiB on the two-phase
         # all-pairs moves fewer HBM bytes (7.5 S vs 9 S per rank) and wins
-        spec = [(0, 4 << 10, 1, "o"), (4 << 10, 2 << 20, 16, "o"), (2 << 20, 8 << 20, 8, "o"),
-                (8 << 20, (1 << 30) + 1, inst_large)]
+        spec = [(0, 4 << 10, 1, "o"), (4 << 10, 16 << 20, 16, "o"), (16 << 20, (1 << 30) + 1, inst_large)]
     else:
         spec = [(0, 64 << 10, 1), (64 << 10, (1 << 30) + 1, inst_large)]
     tiers = []
