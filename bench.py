@@ -89,9 +89,11 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
     minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
     ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
     for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
-    inst_large.  At more ranks: two-phase all-pairs, 1 instance below 64 KiB, inst_large above."""
+    inst_large.  At more ranks: rank-ordered one-shot (4 instances) below 16 KiB, then two-phase
+    all-pairs, 1 instance below 64 KiB, inst_large above."""
     if tiers_arg:
-        # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot
+        # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
+        # "O" = rank-ordered one-shot
         spec = []
         for t in tiers_arg.split(","):
             f = t.split(":")
@@ -102,13 +104,17 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         # all-pairs moves fewer HBM bytes (7.5 S vs 9 S per rank) and wins
         spec = [(0, 4 << 10, 1, "o"), (4 << 10, 16 << 20, 16, "o"), (16 << 20, (1 << 30) + 1, inst_large)]
     else:
-        spec = [(0, 64 << 10, 1), (64 << 10, (1 << 30) + 1, inst_large)]
+        # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 16 KiB: 8 ranks
+        # on one MI355X, fp16, 128 B 23.2 -> 19.5 us (profiles/r01_tier_sweep8.txt); it moves
+        # (n-1) S per rank, so the two-phase schedule takes over early
+        spec = [(0, 16 << 10, 4, "O"), (16 << 10, 64 << 10, 1), (64 << 10, (1 << 30) + 1, inst_large)]
     tiers = []
     for k, t in enumerate(spec):
         lo, hi, inst = t[:3]
         kind = t[3] if len(t) > 3 else "a"
-        if kind == "o":
-            x = xmlgen.allreduce_oneshot(n, inst, proto, lo, hi, name="oneshot_t%d_i%d" % (k, inst))
+        if kind in ("o", "O"):
+            x = xmlgen.allreduce_oneshot(n, inst, proto, lo, hi, name="oneshot_t%d_i%d" % (k, inst),
+                                         ordered=kind == "O")
         else:
             x = xmlgen.allreduce_allpairs(n, inst, proto, True, lo, hi, name="allpairs_t%d_i%d" % (k, inst))
         pth = os.path.join(tmp, "bench_ap%d_%s_t%d_i%d_%s_%d.xml" % (n, proto, k, inst, kind, os.getpid()))
@@ -357,7 +363,7 @@ def main():
     for nbytes in sizes:
         cnt = nbytes // ts
         tier = tier_of(tiers, nbytes)
-        ncpl = tier[2] * (n * n if tier[4] == "a" else 1)
+        ncpl = tier[2] * (n * n if tier[4] == "a" else 1)  # one-shot: instances
         if cnt % ncpl:
             continue
         for _ in range(a.warmup):
@@ -448,7 +454,7 @@ def main():
         "config": {"workload": workload,
                    "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
-                   "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot"}[t[4]]] for t in tiers],
+                   "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot", "O": "oneshot-ordered"}[t[4]]] for t in tiers],
                    "launch": "hipgraph" if a.graph else "eager",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),

@@ -153,15 +153,21 @@ def allreduce_allpairs(n: int, instances: int = 1, proto: str = "LL", inplace: b
 
 def allreduce_oneshot(n: int, instances: int = 1, proto: str = "LL",
                       min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
-                      nthreads: Optional[int] = None, name: str = "allreduce_oneshot") -> str:
+                      nthreads: Optional[int] = None, name: str = "allreduce_oneshot",
+                      ordered: bool = False) -> str:
     """One-shot all-pairs AllReduce (in place): every rank sends its whole buffer to every peer's
-    scratch, then reduces the n-1 received copies into its own buffer.  Three transfers on the
-    critical path (s, r, re) instead of the two-phase schedule's seven, for latency-bound sizes.
-    Each rank folds its own data first (re: d (+) s_p), so for n == 2 and a commutative op both
-    ranks hold the same bits; for n > 2 ranks may differ in floating-point rounding."""
+    scratch, then reduces the received copies.  Fewer transfers on the critical path than the
+    two-phase schedule (s, r, re instead of s, r, re, s, r), for latency-bound sizes.
+    ordered=False: re folds the n-1 received copies into the rank's own buffer, d (+) s_p; for
+      n == 2 and a commutative op both ranks hold the same bits, for n > 2 ranks may differ in
+      floating-point rounding.
+    ordered=True: rank q's data sits in scratch slot q on every rank (own data by a local cpy),
+      re folds slots 1..n-1 into slot 0 and a cpy writes the result back, so every rank folds in
+      rank order and all ranks hold the same bits for any n (one transfer more: s, r, re, cpy)."""
     if n < 2:
         raise ValueError("oneshot needs at least 2 ranks")
     I = instances
+    nslot = n if ordered else n - 1
     gpus = {}
     for r in range(n):
         peers = [p for p in range(n) if p != r]
@@ -170,21 +176,32 @@ def allreduce_oneshot(n: int, instances: int = 1, proto: str = "LL",
         for pi, p in enumerate(peers):
             for k in range(I):
                 tb = _Tb(I + pi * I + k, p, p, k)
-                tb.add("s", "i", k, "s", k * (n - 1) + _slot_of(r, p), 1)
-                tb.add("r", "i", k, "s", k * (n - 1) + pi, 1, hasdep=1)
+                rs = k * nslot + (p if ordered else pi)
+                tb.add("s", "i", k, "s", k * nslot + (r if ordered else _slot_of(r, p)), 1)
+                tb.add("r", "i", k, "s", rs, 1, hasdep=1)
                 ptb[(k, p)] = tb
         for k in range(I):
             tb = red[k]
             others = [ptb[(k, p)].id for p in peers]
+            if ordered:
+                tb.add("cpy", "i", k, "s", k * n + r, 1)
             for dep in others[1:]:
                 tb.nop(dep, 1)
-            for pi, p in enumerate(peers):
-                if pi == 0:
-                    tb.add("re", "s", k * (n - 1) + pi, "i", k, 1, others[0], 1)
-                else:
-                    tb.add("re", "s", k * (n - 1) + pi, "i", k, 1)
+            if ordered:
+                for q in range(1, n):
+                    if q == 1:
+                        tb.add("re", "s", k * n + q, "s", k * n, 1, others[0], 1)
+                    else:
+                        tb.add("re", "s", k * n + q, "s", k * n, 1)
+                tb.add("cpy", "s", k * n, "i", k, 1)
+            else:
+                for pi, p in enumerate(peers):
+                    if pi == 0:
+                        tb.add("re", "s", k * (n - 1) + pi, "i", k, 1, others[0], 1)
+                    else:
+                        tb.add("re", "s", k * (n - 1) + pi, "i", k, 1)
         tbs = red + [ptb[(k, p)] for p in peers for k in range(I)]
-        gpus[r] = (I, 0, I * (n - 1), tbs)
+        gpus[r] = (I, 0, I * nslot, tbs)
     if max_bytes is None:
         max_bytes = 1 << 62
     return _emit(name, proto, I, I, n, "allreduce", True, gpus, min_bytes, max_bytes, nthreads)

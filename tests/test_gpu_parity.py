@@ -57,6 +57,23 @@ def test_oneshot_allreduce(proto, n, inst, count, dt):
 
 
 @pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
+@pytest.mark.parametrize("n,inst,count,dt", [
+    (8, 1, 64, 6),              # 128 B fp16 (the C3 sweep's first point)
+    (8, 4, 4 * 5003, 6),
+    (4, 16, 16 * 4096, 9),
+    (3, 2, 2 * 777, 7),
+])
+def test_oneshot_ordered_allreduce(proto, n, inst, count, dt):
+    """Rank-ordered one-shot vs the oracle, bit-exact, and the same bits on every rank."""
+    from tests.gpu_harness import run_collective
+    xml = xmlgen.allreduce_oneshot(n, inst, proto, ordered=True)
+    check(xml, n, L.ALLREDUCE, count, dt)
+    gpu, _, _ = run_collective(xml, n, L.ALLREDUCE, count, dt, 0, True, 5, "uniform", 1)
+    for r in range(1, n):
+        assert np.array_equal(gpu[0].view(np.uint8), gpu[r].view(np.uint8))
+
+
+@pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
 def test_allpairs_out_of_place(proto):
     check(xmlgen.allreduce_allpairs(8, 2, proto, inplace=False), 8, L.ALLREDUCE, 128 * 513, 7, inplace=False)
 

@@ -32,6 +32,8 @@ def run(xml, n, coll, count, dt, op=0, inplace=True, mode="exact", seed=1):
     (lambda: xmlgen.allreduce_oneshot(2, 1, "LL"), 2, 33, 7, True),
     (lambda: xmlgen.allreduce_oneshot(2, 4, "Simple"), 2, 4 * 1000, 7, True),
     (lambda: xmlgen.allreduce_oneshot(4, 2, "LL128"), 4, 2 * 300, 6, True),
+    (lambda: xmlgen.allreduce_oneshot(8, 2, "LL", ordered=True), 8, 2 * 500, 7, True),
+    (lambda: xmlgen.allreduce_oneshot(3, 1, "Simple", ordered=True), 3, 1000, 9, True),
 ])
 def test_allreduce_exact_sum(xml, n, count, dt, inplace):
     ins, outs = run(xml(), n, L.ALLREDUCE, count, dt, inplace=inplace)
@@ -46,6 +48,22 @@ def test_oneshot_two_ranks_bitwise_identical_across_ranks():
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
     want = N.apply(0, 7, ins[0], ins[1])  # fp32 a + b, RNE
     assert np.array_equal(outs[0].view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
+
+
+@pytest.mark.parametrize("proto", ["LL", "LL128", "Simple"])
+def test_oneshot_ordered_rank_order_fold(proto):
+    """ordered one-shot: every rank holds the same bits, the left fold x0 (+) x1 (+) ... in rank
+    order (LL / LL128: dst first; Simple: (s1 (+) ... ) (+) d, the same on every rank)."""
+    n, dt = 5, 7
+    ins, outs = run(xmlgen.allreduce_oneshot(n, 2, proto, ordered=True), n, L.ALLREDUCE, 2 * 999, dt,
+                    mode="uniform")
+    for r in range(1, n):
+        assert np.array_equal(outs[0].view(np.uint32), outs[r].view(np.uint32))
+    if proto != "Simple":
+        want = ins[0]
+        for q in range(1, n):
+            want = N.apply(0, dt, want, ins[q])
+        assert np.array_equal(outs[0].view(np.uint32), np.asarray(want, np.float32).view(np.uint32))
 
 
 def test_reduce_scatter_allgather_exact():
