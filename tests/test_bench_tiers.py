@@ -1,0 +1,43 @@
+"""bench.py's schedule tiers: contiguous cover of the sweep, at most MSCCL_MAX_NUM_ALGOS (4) XMLs,
+every XML valid on every rank (product loader), and every default sweep size divisible by its
+tier's nchunksperloop, so no sweep point is silently skipped (CPU only)."""
+import sys
+
+import pytest
+
+import msccl_amd as M
+
+
+@pytest.fixture(scope="module")
+def bench():
+    argv = sys.argv
+    sys.argv = ["bench.py"]
+    try:
+        import bench as B
+    finally:
+        sys.argv = argv
+    return B
+
+
+@pytest.mark.parametrize("n,inst,ts", [(2, 16, 4), (4, 8, 4), (8, 4, 2)])
+def test_default_tiers_cover_the_sweep(bench, tmp_path, n, inst, ts):
+    tiers = bench.make_xmls(n, "LL", inst, str(tmp_path))
+    assert 1 <= len(tiers) <= 4
+    assert tiers[0][0] == 0
+    for a, b in zip(tiers, tiers[1:]):
+        assert a[1] == b[0]
+    assert tiers[-1][1] > max(bench.SIZES)
+    for lo, hi, i, path, kind in tiers:
+        for r in range(n):
+            j = M.algo_json(path, r, n)
+            assert j["valid"] == 1 and j["minBytes"] == lo and j["maxBytes"] == hi
+    for nbytes in bench.SIZES:
+        t = bench.tier_of(tiers, nbytes)
+        ncpl = t[2] * (n * n if t[4] == "a" else 1)
+        assert (nbytes // ts) % ncpl == 0, (nbytes, t)
+
+
+def test_tier_spec_with_kinds(bench, tmp_path):
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path), "0:4096:1:o,4096:65536:2:O,65536:1073741825:4")
+    assert [t[4] for t in tiers] == ["o", "O", "a"]
+    assert [t[2] for t in tiers] == [1, 2, 4]
