@@ -54,6 +54,13 @@ __device__ __forceinline__ uint64_t computeFlag(uint64_t workIndex, uint64_t ite
 // are a contiguous 1 KiB.
 __device__ __forceinline__ int llLineIdx(int p, int h) { return ((p >> 6) << 7) + (h << 6) + (p & 63); }
 
+// a / b for a >= 0, b > 0: a shift when b is a power of two (the usual case for chunk and split
+// sizes), so the iteration prologue does not pay for 64-bit software divisions
+__device__ __forceinline__ int64_t divNonNeg(int64_t a, int64_t b) {
+  if ((b & (b - 1)) == 0) return a >> (63 - __builtin_clzll((uint64_t)b));
+  return a / b;
+}
+
 // The packs of one primitive call that this workgroup owns: `count` chunks of Q packs each,
 // positions [q0, q0 + Lq) of every chunk.  Sub-local pack s maps to op pack bufPack(s).
 struct Shape {
@@ -792,9 +799,9 @@ struct Interp {
         nelemGrid = loop;
       } else if constexpr (PROTO == pSimple) {
         real = sizePer - grid < chunkSize ? sizePer - grid : chunkSize;
-        real = (real + w.minChunk - 1) / w.minChunk * w.minChunk;
+        real = divNonNeg(real + w.minChunk - 1, w.minChunk) * w.minChunk;
       } else {
-        int64_t rem = (sizePer - grid + w.minChunk - 1) / w.minChunk * w.minChunk;
+        int64_t rem = divNonNeg(sizePer - grid + w.minChunk - 1, w.minChunk) * w.minChunk;
         real = rem < chunkSize ? rem : chunkSize;
       }
       int nelem = 0;
@@ -811,7 +818,7 @@ struct Interp {
       // this workgroup's positions inside every chunk of this iteration (nelem % PE == 0
       // whenever split > 1: the host sets split = 1 otherwise)
       const int Qc = (nelem + PE - 1) / PE;
-      const int q0 = (int)((int64_t)Qc * sub / split), q1 = (int)((int64_t)Qc * (sub + 1) / split);
+      const int q0 = (int)divNonNeg((int64_t)Qc * sub, split), q1 = (int)divNonNeg((int64_t)Qc * (sub + 1), split);
       int step = 0;
       for (int i = 0; i < hd.nsteps; i++) {
         DevTransfer t;
