@@ -12,6 +12,7 @@
 #include "../../include/nccl.h"
 #include "algo.h"
 #include "device/devcomm.h"
+#include "plan.h"
 
 namespace msccl {
 
@@ -52,9 +53,12 @@ struct ncclComm {
   std::vector<msccl::Registration> regs;
   std::vector<msccl::DevAlgoHost> devAlgos;
   msccl::DevAlgoHost ringAlgos[4];  // ring fallback programs (transport.cc: ringUpload)
+  msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank
   bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank
-  std::vector<int> algoSplit;
-  std::vector<int> algoSendRun;    // per algorithm: longest run of send chunks before a receive (any tb)      // workgroups per XML thread block, per algorithm (same on all ranks)
+  bool anyRemote = false;          // some peer runs on another GPU (xGMI): no LL128 unless allowed
+  std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
+  std::vector<int> algoSendRun;    // per algorithm: longest run of send chunks before a receive, max over
+                                   // every rank's program (same on all ranks)
   int maxSplit = 1;                // sub-connections per (channel, peer)
   int coResident = 1;              // ranks of this communicator on this rank's GPU
 
@@ -92,6 +96,11 @@ struct ncclComm {
   msccl::Bootstrap* boot = nullptr;
   bool ownsBoot = false;
 
+  // what the most recent collective ran (introspection: mscclAmdCommInfo "last")
+  struct LastLaunch {
+    int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0;
+  } last;
+
   hipStream_t userStream = nullptr;
   bool userStreamSet = false;
   hipEvent_t doneEvent = nullptr;
@@ -110,6 +119,7 @@ ncclResult_t transportPlan(ncclComm* comm);                 // keys, arena layou
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
                               const std::vector<char*>& peerBases, const std::vector<int>& peerRemote);
 ncclResult_t algoUpload(ncclComm* comm);
+int algoSendRunOf(const Algorithm& a);
 ncclResult_t ringUpload(ncclComm* comm);
 
 // enqueue.cc

@@ -44,12 +44,13 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
   c.rank = rank;
   c.inPlace = inPlace != 0;
   std::vector<Registration> regs;
-  int idx = selectAlgo(algos, regs, c);
+  const Knobs k = Knobs::fromEnv();
+  int idx = selectAlgo(algos, regs, c, k);
   std::ostringstream o;
   if (idx < 0) {
     o << "{\"algo\":-1,\"nalgos\":" << algos.size();
     Plan rp;
-    if (envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0 && nranks > 1 && makeRingPlan(c, &rp) == 0)
+    if (k.ringFallback && nranks > 1 && makeRingPlan(c, k, &rp) == 0)
       o << ",\"ring\":{\"coll\":" << rp.ringColl << ",\"proto\":" << rp.proto << ",\"channels\":" << rp.ringChannels
         << ",\"nthreads\":" << rp.refNthreads << ",\"size\":" << rp.count << ",\"dtype\":" << rp.dtype
         << ",\"nBytes\":" << rp.nBytes << ",\"chunk\":" << rp.chunkSize << ",\"minChunk\":" << rp.minChunk
@@ -58,7 +59,7 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
     return putOut(o.str(), out, outLen);
   }
   Plan p;
-  int r = makePlan(algos, idx, -1, c, &p);
+  int r = makePlan(algos, idx, -1, c, k, &p);
   if (r != 0) return r;
   o << "{\"algo\":" << idx << ",\"nalgos\":" << algos.size() << ",\"proto\":" << p.proto
     << ",\"nthreads\":" << p.refNthreads << ",\"count\":" << p.count << ",\"dtype\":" << p.dtype
@@ -84,9 +85,15 @@ int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
     << ",\"arenaBytes\":" << comm->arenaSize << ",\"scratchBytes\":" << comm->scratchSize
     << ",\"llSlotLines\":" << comm->llSlotLines << ",\"simpleSlotBytes\":" << comm->simpleSlotBytes
     << ",\"workIndex\":" << comm->workIndex << ",\"maxSplit\":" << comm->maxSplit
-    << ",\"coResident\":" << comm->coResident << ",\"algoSplit\":[";
+    << ",\"coResident\":" << comm->coResident << ",\"anyRemote\":" << (comm->anyRemote ? 1 : 0)
+    << ",\"algoSplit\":[";
   for (size_t i = 0; i < comm->algoSplit.size(); i++) o << (i ? "," : "") << comm->algoSplit[i];
-  o << "]}";
+  o << "],\"algoSendRun\":[";
+  for (size_t i = 0; i < comm->algoSendRun.size(); i++) o << (i ? "," : "") << comm->algoSendRun[i];
+  const auto& L = comm->last;
+  o << "],\"last\":{\"algo\":" << L.algo << ",\"proto\":" << L.proto << ",\"split\":" << L.split
+    << ",\"merge\":" << L.merge << ",\"ringColl\":" << L.ringColl << ",\"ringChannels\":" << L.ringChannels
+    << ",\"blocks\":" << L.blocks << "}}";
   return putOut(o.str(), out, outLen);
 }
 

@@ -100,7 +100,7 @@ struct DevComm {
   uint64_t* flags;              // [kFlagSlots * kFlagStride]
   volatile uint32_t* abortFlag; // host-mapped
   uint32_t* errWord;            // host-mapped: 0 ok, else error code (1 timeout, 2 bad program)
-  uint64_t timeoutTicks;        // s_memrealtime ticks (100 MHz)
+  uint64_t timeoutTicks;        // s_memrealtime ticks (100 MHz) a single wait may last; 0 = for ever
   int32_t maxSplit;             // sub-connections per (channel, peer): conn k of key c = send[c*maxSplit+k]
   int32_t pad;
   // Launch epoch (the reference's host-side workIndex, enqueue.cc:714-721, kept on the device so
@@ -116,6 +116,13 @@ struct DevComm {
   struct TraceEvent* trace;
   int32_t traceEvents;
   int32_t pad2;
+  // LL / LL128 flag arithmetic (devcomm.h:56-63): flag = (step + 1) & llFlagMask, and a sender
+  // stamps the unused lines of a slot on steps with (step & llCleanMask) == llCleanMask.
+  // Production: 0xffffffff / 0x7ffffff8.  MSCCL_AMD_TEST_LL_CLEANUP=1 is the reference's
+  // TEST_LL_CLEANUP build (NCCL_LL_FLAG_MAX 0x100, NCCL_LL_CLEAN_MASK 0x078): the flag wraps every
+  // 256 steps and the cleanup runs 8 steps in every 128, so tests reach it in a few launches.
+  uint32_t llFlagMask;
+  uint32_t llCleanMask;
 };
 
 // Ring fallback kinds (RankWork::ringColl)
@@ -168,6 +175,7 @@ enum : uint32_t { kDevOk = 0, kDevTimeout = 1, kDevAbort = 2, kDevBadOp = 3 };
 
 // Host-side kernel dispatch (kernels.hip)
 typedef int (*LaunchFn)(const LaunchArgs& args, int gridBlocks, void* stream);
+constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = resident workgroups per CU
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
 
 }  // namespace msccl

@@ -30,7 +30,6 @@ namespace msccl {
 
 enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7, tCopySend = 9 };
 enum : int { pLL = 0, pLL128 = 1, pSimple = 2 };
-constexpr uint64_t kLLCleanMask = 0x7ffffff8ull;  // NCCL_LL_CLEAN_MASK (devcomm.h:61)
 
 struct alignas(16) BlockShared {
   DevTransfer tr[256];
@@ -91,6 +90,9 @@ struct Interp {
   uint64_t sendStep, recvStep;
   uint64_t headSeen, tailSeen;  // credit / Simple data known available without polling
   uint64_t t0;
+  uint64_t timeoutTicks;  // 0 = wait for ever (DevComm::timeoutTicks)
+  uint32_t llFlagMask;    // LL / LL128 flag = (step + 1) & llFlagMask (NCCL_LL_FLAG, devcomm.h:56-63)
+  uint32_t llCleanMask;   // cleanup steps: (step & mask) == mask (NCCL_LL_CLEAN_MASK)
   int tid;
   int refNthreads;
   TraceEvent* trace;  // this workgroup's trace slot (null = tracing off)
@@ -108,15 +110,30 @@ struct Interp {
   }
 
   // ---------------------------------------------------------------- spins / abort
-  __device__ __forceinline__ bool spinAbort(uint32_t& spins) {
-    if ((++spins & 1023u) != 0) return false;
+  // Every poll loop owns a Spin.  Each 1024 polls check the host-mapped abort word
+  // (ncclCommAbort) and, when MSCCL_AMD_TIMEOUT_SEC > 0, how long THIS wait has lasted (the
+  // clock starts at the wait's first check, not at the launch).  The default, 0, waits for ever
+  // as the reference does (prims_*.h checkAbort only polls the abort flag).  On abort or timeout
+  // the error is recorded for ncclCommGetAsyncError and every later wait of the workgroup gives
+  // up at once; the host then refuses further collectives on the communicator (enqueue.cc).
+  struct Spin {
+    uint32_t n = 0;
+    uint64_t start = 0;
+  };
+  __device__ __forceinline__ bool spinAbort(Spin& sp) {
+    if ((++sp.n & 1023u) != 0) return false;
     if (sh->aborted) return true;
     uint32_t code = kDevOk;
-    if (*comm->abortFlag) code = kDevAbort;
-    else if (__builtin_amdgcn_s_memrealtime() - t0 > comm->timeoutTicks) code = kDevTimeout;
+    if (atomicLoadSys32(comm->abortFlag)) {
+      code = kDevAbort;
+    } else if (timeoutTicks != 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (sp.n == 1024u) sp.start = now;
+      else if (now - sp.start > timeoutTicks) code = kDevTimeout;
+    }
     if (code != kDevOk) {
       sh->aborted = 1;
-      __hip_atomic_store(comm->errWord, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      atomicStoreSys32(comm->errWord, code);
       return true;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -130,7 +147,7 @@ struct Interp {
   __device__ __forceinline__ void waitSendCredit() {
     if (headSeen + SLOTS >= sendStep + 1) return;
     if (tid == 0) {
-      uint32_t spins = 0;
+      Spin spins;
       uint64_t h;
       while ((h = atomicLoadSys(sc->head)) + SLOTS < sendStep + 1) {
         if (spinAbort(spins)) break;
@@ -144,7 +161,7 @@ struct Interp {
   __device__ __forceinline__ void waitRecvTail() {
     if (tailSeen >= recvStep + 1) return;
     if (tid == 0) {
-      uint32_t spins = 0;
+      Spin spins;
       uint64_t t;
       while ((t = atomicLoadSys(rc->tail)) < recvStep + 1) {
         if (spinAbort(spins)) break;
@@ -226,11 +243,11 @@ struct Interp {
       uint32_t rflag = 0, sflag = 0;
       if (RECV) {
         rslot = rc->ll + (recvStep % kLLFifoSlots) * (uint64_t)rc->llSlotLines;
-        rflag = (uint32_t)(recvStep + 1);
+        rflag = (uint32_t)(recvStep + 1) & llFlagMask;
       }
       if (SEND) {
         frs = makeRsrc(sc->ll + (sendStep % kLLFifoSlots) * (uint64_t)sc->llSlotLines);
-        sflag = (uint32_t)(sendStep + 1);
+        sflag = (uint32_t)(sendStep + 1) & llFlagMask;
       }
       if constexpr (kL16) {
         l16Step<RECV, SEND, SRC, DST>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1);
@@ -238,7 +255,7 @@ struct Interp {
         llStep<RECV, SEND, SRC, DST>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1, nlinesFull);
       }
       if (SEND) {
-        if ((sendStep & kLLCleanMask) == kLLCleanMask) {
+        if ((sendStep & llCleanMask) == llCleanMask) {
           // LL cleanup (prims_ll.h:90-97): stamp every unused line of the slot with this flag
           const int units = (s1 - s0 + 2) / 3;
           for (int l = tid; l < slotLines; l += kNT) {
@@ -291,11 +308,11 @@ struct Interp {
       uint32_t rflag = 0, sflag = 0;
       if (RECV) {
         rslot = rc->ll + (recvStep % kLLFifoSlots) * (uint64_t)rc->llSlotLines;
-        rflag = (uint32_t)(recvStep + 1);
+        rflag = (uint32_t)(recvStep + 1) & llFlagMask;
       }
       if (SEND) {
         frs = makeRsrc(sc->ll + (sendStep % kLLFifoSlots) * (uint64_t)sc->llSlotLines);
-        sflag = (uint32_t)(sendStep + 1);
+        sflag = (uint32_t)(sendStep + 1) & llFlagMask;
       }
       const int nLines = (u1 - u0) * 4;
       for (int base = tid; base < nLines; base += kNT * UL) {
@@ -339,7 +356,7 @@ struct Interp {
           ldLines4(la, ln);
 #pragma unroll
           for (int k = 0; k < UL; k++) {
-            uint32_t spins = 0;
+            Spin spins;
             while (has[k] && ln[k].w != rflag) {
               if (spinAbort(spins)) break;
               ldLine1(la[k], ln[k]);
@@ -367,7 +384,7 @@ struct Interp {
         }
       }
       if (SEND) {
-        if ((sendStep & kLLCleanMask) == kLLCleanMask) {
+        if ((sendStep & llCleanMask) == llCleanMask) {
           // LL cleanup (prims_ll.h:90-97): stamp every line of the slot that carries no payload
           for (int l = tid; l < slotLines; l += kNT) {
             const int u = u0 + (l >> 2), j = l & 3;
@@ -450,7 +467,7 @@ struct Interp {
         ldLines8(la, ln);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-          uint32_t spins = 0;
+          Spin spins;
           while (act[u] && (ln[2 * u].y != rflag || ln[2 * u].w != rflag || ln[2 * u + 1].y != rflag ||
                             ln[2 * u + 1].w != rflag)) {
             if (spinAbort(spins)) break;
@@ -520,7 +537,7 @@ struct Interp {
 #pragma unroll
         for (int k = 0; k < UU; k++) {
           const int nl = nv[k] > 0 ? l16Lines(nv[k]) : 0;
-          uint32_t spins = 0;
+          Spin spins;
           while ((nl > 0 && ln[4 * k].w != rflag) || (nl > 1 && ln[4 * k + 1].w != rflag) ||
                  (nl > 2 && ln[4 * k + 2].w != rflag) || (nl > 3 && ln[4 * k + 3].w != rflag)) {
             if (spinAbort(spins)) break;
@@ -711,6 +728,9 @@ struct Interp {
     comm = w.comm;
     refNthreads = w.refNthreads;
     t0 = __builtin_amdgcn_s_memrealtime();
+    timeoutTicks = uni(comm->timeoutTicks);
+    llFlagMask = uni(comm->llFlagMask);
+    llCleanMask = uni(comm->llCleanMask);
     const int split = w.split;
     const int maxSplit = w.maxSplit;
     const int slot = bid * maxSplit + sub;  // flag / epoch / trace slot of this workgroup
@@ -832,7 +852,7 @@ struct Interp {
           if (tid < t.numDeps) {
             const int db = sh->depBid[t.depPtr + tid];
             const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)sh->depStep[t.depPtr + tid]);
-            uint32_t spins = 0;
+            Spin spins;
             while (true) {
               uint64_t cur = atomicLoadAgent(flags + ((size_t)db * maxSplit + sub) * kFlagStride);
               if (cur >= goal && (cur >> 24) == workIndex) break;
@@ -849,8 +869,18 @@ struct Interp {
         // (enqueue.cc:700-711); these primitives cut calls into FIFO steps themselves, so when the
         // iteration covers whole chunks (consecutive chunks are contiguous) a transfer's chunks
         // move as one call.  Not for `re`: its per-element path depends on the call's size.
-        const int macT = (t.type != tRe && !ringColl && nelem == sizePer &&
-                          (t.type != tSend || (int64_t)nelem * t.count <= w.maxOpElems)) ? t.count : mac;
+        // The rule depends only on (nelem, count), which the two ends of a connection share, so
+        // a sender and its receiver cut the same calls and hence the same FIFO steps (a sender
+        // splitting a transfer its receiver moves whole would misalign the steps whenever a call
+        // is not a whole number of slots).  Calls stay within kMaxRunSlots slots per
+        // sub-connection, and so far below the 2 GiB reach of a buffer descriptor.
+        int macT = (t.type != tRe && !ringColl && nelem == sizePer &&
+                    (int64_t)nelem * t.count <= w.maxOpElems) ? t.count : mac;
+        {
+          // buffer descriptors address 2^31 - 1 bytes from a call's base (makeRsrc)
+          const int64_t reach = nelem > 0 ? (int64_t)0x7fffff00 / ((int64_t)nelem * TS) : 1;
+          if (macT > reach) macT = reach < 1 ? 1 : (int)reach;
+        }
         for (int c = 0; c < t.count; c += macT) {
           int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
           int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;

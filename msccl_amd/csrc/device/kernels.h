@@ -5,8 +5,16 @@
 
 namespace msccl {
 
+// gridBlocks > 0: launch, returns 0 on success.  gridBlocks == kQueryResidency: returns how many
+// workgroups of this kernel one CU holds at once (0 on error), which bounds a co-resident launch:
+// every workgroup of a launch spins on others, so all of them must be resident together.
 template <typename T, int OP, int PROTO>
 int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  if (gridBlocks == kQueryResidency) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclKernel<T, OP, PROTO>, kNT, 0) != hipSuccess) return 0;
+    return n;
+  }
   hipLaunchKernelGGL((mscclKernel<T, OP, PROTO>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, args);
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }

@@ -74,10 +74,10 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   c.inPlace = inPlaceOf(op.coll, op.sendbuff, op.recvbuff, op.count, op.dtype, comm->rank);
   c.customAlgo = op.customAlgo;
   out->inPlace = c.inPlace;
-  int idx = selectAlgo(comm->algos, comm->regs, c);
+  int idx = selectAlgo(comm->algos, comm->regs, c, comm->knobs);
   if (idx < 0) {
     // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
-    if (comm->ringFallback && makeRingPlan(c, &out->plan) == 0) {
+    if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
       INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; ring fallback (%s, %d channels)",
            op.coll, op.count, (int)op.dtype, out->plan.proto == kProtoLL ? "LL" : "Simple", out->plan.ringChannels);
       return ncclSuccess;
@@ -90,8 +90,30 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   int protoOverride = -1;
   for (auto& r : comm->regs)
     if (r.algoIndex == idx) protoOverride = r.proto;
-  NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, &out->plan));
+  if ((protoOverride >= 0 ? protoOverride : comm->algos[idx].proto) == kProtoLL128 && comm->anyRemote &&
+      !comm->knobs.ll128Remote) {
+    // The CDNA4 LL128 line relies on a 16-B store arriving untorn.  That is observed for local
+    // HBM, not shown for xGMI peer stores; the reference likewise enables LL128 only where its
+    // line atomicity holds (tuning.cc:210-214).  Run the schedule with LL (same values for the
+    // commutative ops MSCCL admits) unless MSCCL_AMD_LL128_REMOTE=1.
+    static bool warned = false;
+    if (!warned) {
+      warned = true;
+      WARN("MSCCL: algorithm %s is LL128 and peers are on other GPUs; running it with LL "
+           "(MSCCL_AMD_LL128_REMOTE=1 keeps LL128)", comm->algos[idx].name.c_str());
+    }
+    protoOverride = kProtoLL;
+  }
+  NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, comm->knobs, &out->plan));
   if (out->plan.scratchNeeded > comm->scratchSize) {
+    // The scratch is sized from the XMLs' maxBytes at init (init.cc:809-835), so this only
+    // happens when MSCCL_AMD_MAX_SCRATCH capped it.  The reference reports ncclInternalError
+    // (enqueue.cc:580-589); the capped schedule is treated as not matching instead.
+    if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
+      INFO(kSubColl, "MSCCL: scratch %zu < %zu needed (MSCCL_AMD_MAX_SCRATCH); ring fallback", comm->scratchSize,
+           out->plan.scratchNeeded);
+      return ncclSuccess;
+    }
     WARN("MSCCL: MSCCL scratch pad size is smaller than expected %zu < %zu", comm->scratchSize, out->plan.scratchNeeded);
     return ncclInternalError;
   }
@@ -129,6 +151,7 @@ RankWork makeRingWork(Planned& p) {
   w.ringSize = p.plan.count;
   w.ringLastChunk = p.plan.ringLastChunk;
   w.launchSeq = comm->workIndex++;
+  comm->last = {-1, p.plan.proto, 1, 1, p.plan.ringColl, p.plan.ringChannels, w.nBlocks};
   return w;
 }
 
@@ -159,7 +182,7 @@ RankWork makeWork(Planned& p) {
   if (p.plan.sizePerChunk % pe != 0) split = 1;
   // Small messages: fewer, fuller workgroups (at least one pack per lane of every workgroup);
   // a split forced with MSCCL_AMD_SPLIT is kept as is.
-  if (envInt("MSCCL_AMD_SPLIT", 0) <= 0)
+  if (comm->knobs.split <= 0)
     while (split > 1 && p.plan.sizePerChunk / pe < (int64_t)split * kNT) split /= 2;
   w.split = (uint8_t)split;
   w.nBlocks = (int16_t)(da.nBlocks * split);
@@ -180,17 +203,21 @@ RankWork makeWork(Planned& p) {
   const int64_t sendRun = std::max(1, comm->algoSendRun.empty() ? 1 : comm->algoSendRun[p.plan.algoIndex]);
   int merge = 1;
   if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {
-    const int64_t envMerge = envInt("MSCCL_AMD_MERGE", 0);
+    const int64_t envMerge = comm->knobs.merge;
     // as many full iterations per call as the bound allows: fewest dependency rounds
     // (C2 32 MiB LL: 348 GB/s with `split` iterations per call, 405 with all 16)
-    const int64_t fit = std::max<int64_t>(1, w.maxOpElems / (std::max<int64_t>(1, p.plan.chunkSize) * sendRun));
+    const int64_t chunk = std::max<int64_t>(1, p.plan.chunkSize);
+    const int64_t fit = std::max<int64_t>(1, w.maxOpElems / (chunk * sendRun));
     merge = (int)std::min<int64_t>(envMerge > 0 ? envMerge : fit, fit);  // MSCCL_AMD_MERGE only lowers it
-    merge = std::max(1, std::min(merge, 64));
+    // a merged iteration stays within 1 GiB, far inside a buffer descriptor's 2 GiB reach
+    const int64_t reach = std::max<int64_t>(1, (1ll << 30) / (chunk * refTypeSize(p.plan.dtype)));
+    merge = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)merge, 64, reach}));
   }
   w.merge = (uint8_t)merge;
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.launchSeq = comm->workIndex++;
+  comm->last = {p.plan.algoIndex, p.plan.proto, split, merge, 0, 0, w.nBlocks};
   return w;
 }
 
@@ -221,6 +248,24 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   const Planned& p0 = *ps[0];
   LaunchFn fn = getLaunchFn(p0.plan.dtype, p0.op.op, p0.plan.proto);
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, (int)p0.op.op, p0.plan.proto); return ncclInvalidArgument; }
+  {
+    // Every workgroup of the launch may spin on every other one (FIFO credits, dependency
+    // flags), so all of them must be resident at once: refuse what the GPU cannot hold instead
+    // of launching a grid that can only hang.
+    static std::map<std::pair<int, LaunchFn>, int> cap;
+    auto key = std::make_pair(dev, fn);
+    auto it = cap.find(key);
+    if (it == cap.end()) {
+      int cus = 0;
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      it = cap.emplace(key, cus * fn(args, kQueryResidency, nullptr)).first;
+    }
+    if (it->second > 0 && blocks > it->second) {
+      WARN("MSCCL: launch needs %d co-resident workgroups but device %d holds %d of this kernel at once "
+           "(fewer co-resident ranks, fewer thread blocks or MSCCL_AMD_SPLIT=1)", blocks, dev, it->second);
+      return ncclInvalidUsage;
+    }
+  }
   if (fn(args, blocks, (void*)primary) != 0) {
     WARN("MSCCL: kernel launch failed: %s", hipGetErrorString(hipGetLastError()));
     return ncclUnhandledCudaError;
@@ -284,13 +329,14 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
       if (res != ncclSuccess) break;
       auto& list = kv.second;
       hipSetDevice(std::get<0>(kv.first));
-      for (size_t s = 0; s < list.size() && res == ncclSuccess; s += kMaxLaunchRanks) {
-        if (list.size() > (size_t)kMaxLaunchRanks)
-          WARN("MSCCL: %zu co-resident ranks on device %d exceed one launch (%d); launching in parts",
-               list.size(), std::get<0>(kv.first), kMaxLaunchRanks);
-        std::vector<Planned*> part(list.begin() + s, list.begin() + std::min(list.size(), s + kMaxLaunchRanks));
-        res = launchGroup(part);
+      if (list.size() > (size_t)kMaxLaunchRanks) {
+        // the ranks' workgroups wait on each other: launched in parts they could only time out
+        WARN("MSCCL: %zu co-resident ranks on device %d in one group; one launch carries at most %d",
+             list.size(), std::get<0>(kv.first), kMaxLaunchRanks);
+        res = ncclInvalidUsage;
+        break;
       }
+      res = launchGroup(list);
     }
   }
   hipSetDevice(saved);
@@ -306,6 +352,13 @@ namespace {
 ncclResult_t enqueue(ncclComm* comm, int coll, const void* sendbuff, void* recvbuff, size_t count,
                      ncclDataType_t dtype, ncclRedOp_t op, hipStream_t stream, int customAlgo, const char* name) {
   if (!commValid(comm)) { WARN("%s : invalid communicator", name); return ncclInvalidArgument; }
+  if (comm->hostErr != nullptr && __atomic_load_n(comm->hostErr, __ATOMIC_ACQUIRE) != kDevOk) {
+    // A kernel of this communicator timed out or was aborted and drained: its FIFO step
+    // counters no longer match the peers', so nothing more may run on it.
+    WARN("%s : communicator has an asynchronous error (%u); destroy or abort it", name,
+         __atomic_load_n(comm->hostErr, __ATOMIC_ACQUIRE));
+    return ncclSystemError;
+  }
   if ((int)dtype < 0 || (int)dtype >= ncclNumTypes) { WARN("%s : invalid type %d", name, (int)dtype); return ncclInvalidArgument; }
   if ((int)op < 0 || (int)op > (int)ncclMaxRedOp) { WARN("%s : invalid reduction operation %d", name, (int)op); return ncclInvalidArgument; }
   if ((int)op >= (int)ncclNumOps) { WARN("%s : reduction operation %d unknown to this communicator", name, (int)op); return ncclInvalidArgument; }

@@ -44,8 +44,10 @@ ncclResult_t loadAlgos(ncclComm* comm) {
 ncclResult_t commLocalSetup(ncclComm* comm) {
   NCCLCHECK(hipErr(hipSetDevice(comm->cudaDev), "hipSetDevice"));
   if (comm->nRanks > 1) NCCLCHECK(loadAlgos(comm));
-  comm->timeoutSec = (double)envInt("MSCCL_AMD_TIMEOUT_SEC", 60);
-  comm->ringFallback = envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0;
+  // 0 (default) = waits never time out, as in the reference; > 0 bounds every single wait
+  comm->timeoutSec = (double)std::max<int64_t>(0, envInt("MSCCL_AMD_TIMEOUT_SEC", 0));
+  comm->knobs = Knobs::fromEnv();
+  comm->ringFallback = comm->knobs.ringFallback != 0;
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostErr, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   *comm->hostAbort = 0;
@@ -84,11 +86,16 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
 }
 
 // What every rank contributes to the split decision (all ranks must reach the same splits).
+// It also carries the knobs and the per-algorithm send runs: launch geometry (split, merge,
+// ring channels, protocol gates, FIFO sizes) must be identical on every rank, or the two ends of
+// a connection would cut different FIFO steps.
 struct SplitRecord {
   char host[64];
   char bus[32];
   int32_t nAlgos;
   int32_t nBlocks[kMaxAlgos];
+  int32_t sendRun[kMaxAlgos];
+  Knobs knobs;
 };
 
 SplitRecord makeSplitRecord(ncclComm* comm) {
@@ -98,11 +105,28 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   if (hipDeviceGetPCIBusId(s.bus, sizeof(s.bus) - 1, comm->cudaDev) != hipSuccess)
     snprintf(s.bus, sizeof(s.bus), "dev%d", comm->cudaDev);
   s.nAlgos = (int32_t)comm->algos.size();
-  for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) s.nBlocks[a] = comm->algos[a].nBlocks;
+  for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) {
+    s.nBlocks[a] = comm->algos[a].nBlocks;
+    s.sendRun[a] = algoSendRunOf(comm->algos[a]);
+  }
+  s.knobs = comm->knobs;
   return s;
 }
 
-void applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
+ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
+  for (size_t r = 0; r < recs.size(); r++) {
+    if (memcmp(&recs[r].knobs, &comm->knobs, sizeof(Knobs)) != 0) {
+      WARN("MSCCL: rank %zu runs with different NCCL_*/MSCCL_AMD_* settings than rank %d (NCCL_ALGO, NCCL_PROTO, "
+           "NCCL_NTHREADS, NCCL_*BUFFSIZE, MSCCL_AMD_SPLIT/MERGE/TARGET_WGS/RING_CHANNELS/RING_FALLBACK/LL128_REMOTE "
+           "must agree)", r, comm->rank);
+      return ncclInvalidUsage;
+    }
+    if (recs[r].nAlgos != (int32_t)comm->algos.size()) {
+      WARN("MSCCL: rank %zu loaded %d MSCCL algorithms, rank %d loaded %zu", r, recs[r].nAlgos, comm->rank,
+           comm->algos.size());
+      return ncclInvalidUsage;
+    }
+  }
   int maxCo = 1;
   for (auto& r : recs) {
     int c = 0;
@@ -113,16 +137,22 @@ void applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   comm->coResident = 0;
   for (auto& q : recs) comm->coResident += !strcmp(mine.host, q.host) && !strcmp(mine.bus, q.bus);
   comm->algoSplit.assign(comm->algos.size(), 1);
+  comm->algoSendRun.assign(comm->algos.size(), 1);
   comm->maxSplit = 1;
   for (size_t a = 0; a < comm->algos.size(); a++) {
-    int mb = 0;
+    int mb = 0, run = 1;
     for (auto& r : recs)
-      if ((int)a < r.nAlgos) mb = std::max(mb, (int)r.nBlocks[a]);
-    comm->algoSplit[a] = chooseSplit(mb, maxCo);
+      if ((int)a < r.nAlgos && a < (size_t)kMaxAlgos) {
+        mb = std::max(mb, (int)r.nBlocks[a]);
+        run = std::max(run, (int)r.sendRun[a]);
+      }
+    comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs);
+    comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
   }
   INFO(kSubInit, "rank %d: %d co-resident ranks per GPU (max), %d sub-connections per connection", comm->rank,
        maxCo, comm->maxSplit);
+  return ncclSuccess;
 }
 
 ncclResult_t commFinish(ncclComm* comm) {
@@ -136,6 +166,9 @@ ncclResult_t commFinish(ncclComm* comm) {
   dc.errWord = comm->devErr;
   dc.timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
   dc.maxSplit = comm->maxSplit;
+  const bool llTest = envInt("MSCCL_AMD_TEST_LL_CLEANUP", 0) != 0;  // TEST_LL_CLEANUP (devcomm.h:56-63)
+  dc.llFlagMask = llTest ? 0xffu : 0xffffffffu;
+  dc.llCleanMask = llTest ? 0x78u : 0x7ffffff8u;
   if (envInt("MSCCL_AMD_TRACE", 0) > 0) {
     comm->traceEvents = (int)std::max<int64_t>(8, std::min<int64_t>(65535, envInt("MSCCL_AMD_TRACE_EVENTS", 256)));
     size_t bytes = (size_t)kMaxTb * comm->maxSplit * comm->traceEvents * sizeof(TraceEvent);
@@ -174,7 +207,7 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
     NCCLCHECK(sb->allgather(&srec, sizeof(srec), &sall));
     std::vector<SplitRecord> recs(n);
     memcpy(recs.data(), sall.data(), sizeof(SplitRecord) * n);
-    applySplits(comm, recs);
+    NCCLCHECK(applySplits(comm, recs));
     NCCLCHECK(transportPlan(comm));
     RankRecord rec;
     memset(&rec, 0, sizeof(rec));
@@ -192,9 +225,11 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
     comm->peerArenaIpc.assign(n, false);
     // a peer is remote (xGMI) unless it runs on the same GPU: same host and PCI bus id
     std::vector<int> peerRemote(n, 0);
-    for (int r = 0; r < n; r++)
+    for (int r = 0; r < n; r++) {
       peerRemote[r] = strcmp(recs[r].host, srec.host) != 0 || strcmp(recs[r].bus, srec.bus) != 0 ||
                       envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;  // test knob: xGMI ordering on one GPU
+      if (r != comm->rank && peerRemote[r]) comm->anyRemote = true;
+    }
     for (int r = 0; r < n; r++) {
       tables[r].resize(comm->table.size());
       memcpy(tables[r].data(), tall.data() + (size_t)r * tbytes, tbytes);
@@ -308,6 +343,19 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   if (hipGetDeviceCount(&ndevices) != hipSuccess) return ncclUnhandledCudaError;
   int saved = 0;
   hipGetDevice(&saved);
+  {
+    // a group of co-resident ranks runs as ONE launch whose workgroups spin on each other;
+    // kMaxLaunchRanks bounds the ranks one launch carries (enqueue.cc: launchGroup)
+    std::vector<int> perDev(std::max(ndevices, 1), 0);
+    for (int i = 0; i < ndev; i++) {
+      int dev = devlist ? devlist[i] : i;
+      if (dev >= 0 && dev < ndevices && ++perDev[dev] > kMaxLaunchRanks) {
+        WARN("ncclCommInitAll : more than %d ranks on device %d; co-resident ranks run in one launch and at most %d "
+             "fit", kMaxLaunchRanks, dev, kMaxLaunchRanks);
+        return ncclInvalidUsage;
+      }
+    }
+  }
   std::vector<ncclComm*> cs(ndev);
   ncclResult_t res = ncclSuccess;
   for (int i = 0; i < ndev && res == ncclSuccess; i++) {
@@ -328,7 +376,8 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
     std::vector<SplitRecord> recs(ndev);
     for (int i = 0; i < ndev; i++) recs[i] = makeSplitRecord(cs[i]);
     for (int i = 0; i < ndev && res == ncclSuccess; i++) {
-      applySplits(cs[i], recs);
+      res = applySplits(cs[i], recs);
+      if (res != ncclSuccess) break;
       hipSetDevice(cs[i]->cudaDev);
       res = transportPlan(cs[i]);
     }
@@ -353,8 +402,10 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
         }
       }
       std::vector<int> remote(ndev);
-      for (int j = 0; j < ndev; j++)
+      for (int j = 0; j < ndev; j++) {
         remote[j] = cs[j]->cudaDev != cs[i]->cudaDev || envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;
+        if (j != i && remote[j]) cs[i]->anyRemote = true;
+      }
       cs[i]->peerArena = bases;
       cs[i]->peerArenaIpc.assign(ndev, false);
       if (res == ncclSuccess) res = transportConnect(cs[i], tables, bases, remote);

@@ -47,28 +47,42 @@ static bool listEnables(const char* str, const char* name, bool def) {
   return invert ? !found : found;
 }
 
-bool mscclEnabled() {
-  // The reference needs NCCL_ALGO to contain MSCCL for AllReduce (tuning.cc:186,217) because
-  // ring/tree exist next to it; here MSCCL is the only algorithm, so it is on unless excluded.
-  return listEnables(getenv("NCCL_ALGO"), "MSCCL", true);
+static int getNthreads(const char* env) {  // NCCL_PARAM-style cached read; -2 = unset
+  return (int)envInt(env, -2);
 }
 
-int chooseSplit(int maxBlocks, int coResident) {
-  int64_t forced = envInt("MSCCL_AMD_SPLIT", 0);
-  int k = 1;
-  if (forced > 0) {
-    while (k * 2 <= kMaxSplit && k * 2 <= forced) k *= 2;
-    return k;
-  }
-  int64_t target = envInt("MSCCL_AMD_TARGET_WGS", 512);
-  int64_t per = (int64_t)std::max(1, maxBlocks) * std::max(1, coResident);
-  while (k * 2 <= kMaxSplit && per * k * 2 <= target) k *= 2;
+Knobs Knobs::fromEnv() {
+  Knobs k;
+  memset(&k, 0, sizeof(k));
+  // The reference needs NCCL_ALGO to contain MSCCL for AllReduce (tuning.cc:186,217) because
+  // ring/tree exist next to it; here MSCCL is the primary algorithm, so it is on unless excluded.
+  k.mscclOn = listEnables(getenv("NCCL_ALGO"), "MSCCL", true);
+  static const char* names[3] = {"LL", "LL128", "Simple"};
+  for (int p = 0; p < 3; p++) k.protoOn[p] = listEnables(getenv("NCCL_PROTO"), names[p], true);
+  k.nthreads = getNthreads("NCCL_NTHREADS");
+  k.ll128Nthreads = getNthreads("NCCL_LL128_NTHREADS");
+  k.buffSizes[kProtoLL] = envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16);
+  k.buffSizes[kProtoLL128] = envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8);
+  k.buffSizes[kProtoSimple] = envInt("NCCL_BUFFSIZE", 1 << 22);
+  k.ringChannels = (int32_t)envInt("MSCCL_AMD_RING_CHANNELS", 0);
+  k.split = (int32_t)envInt("MSCCL_AMD_SPLIT", 0);
+  k.targetWgs = (int32_t)envInt("MSCCL_AMD_TARGET_WGS", 512);
+  k.merge = (int32_t)envInt("MSCCL_AMD_MERGE", 0);
+  k.ringFallback = envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0;
+  k.ll128Remote = envInt("MSCCL_AMD_LL128_REMOTE", 0) != 0;
   return k;
 }
 
-bool protoEnabled(int proto) {
-  static const char* names[3] = {"LL", "LL128", "Simple"};
-  return listEnables(getenv("NCCL_PROTO"), names[proto], true);
+int chooseSplit(int maxBlocks, int coResident, const Knobs& kn) {
+  int k = 1;
+  if (kn.split > 0) {
+    while (k * 2 <= kMaxSplit && k * 2 <= kn.split) k *= 2;
+    return k;
+  }
+  const int64_t target = kn.targetWgs;
+  int64_t per = (int64_t)std::max(1, maxBlocks) * std::max(1, coResident);
+  while (k * 2 <= kMaxSplit && per * k * 2 <= target) k *= 2;
+  return k;
 }
 
 static void argsCheck(const CallDesc& c, int64_t* count, int* dtype, int64_t* nBytes) {
@@ -82,15 +96,16 @@ static void argsCheck(const CallDesc& c, int64_t* count, int* dtype, int64_t* nB
   if (c.coll == kAllGather || c.coll == kReduceScatter || c.coll == kAllToAll) *nBytes *= c.nRanks;
 }
 
-int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c) {
+int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c,
+               const Knobs& k) {
   if (!(c.redop == 0 || c.redop == 1 || c.redop == 2 || c.redop == 3)) return -1;  // tuning.cc:345
-  if (!mscclEnabled()) return -1;
+  if (!k.mscclOn) return -1;
   int64_t count, nBytes;
   int dt;
   argsCheck(c, &count, &dt, &nBytes);
   int64_t total = (c.coll == kAllToAll || c.coll == kAllGather || c.coll == kReduceScatter) ? count * c.nRanks : count;
   auto ok = [&](const Algorithm& a) {
-    return a.valid && protoEnabled(a.proto) && a.coll == c.coll && a.inPlace == (int)c.inPlace &&
+    return a.valid && k.protoOn[a.proto] && a.coll == c.coll && a.inPlace == (int)c.inPlace &&
            a.ngpus == c.nRanks && a.nchunksPerLoop > 0 && total % a.nchunksPerLoop == 0;
   };
   if (c.customAlgo >= 0) {
@@ -100,7 +115,7 @@ int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registrati
   if (!regs.empty()) {  // MSCCL_CONFIG registrations (tuning.cc:350-363)
     for (auto& r : regs) {
       if (r.minBytes <= nBytes && (nBytes < r.maxBytes || r.maxBytes == -1)) {
-        if (r.algoIndex < (int)algos.size() && ok(algos[r.algoIndex]) && protoEnabled(r.proto)) return r.algoIndex;
+        if (r.algoIndex < (int)algos.size() && ok(algos[r.algoIndex]) && k.protoOn[r.proto]) return r.algoIndex;
       }
     }
     return -1;
@@ -112,32 +127,31 @@ int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registrati
   return -1;
 }
 
-static int getNthreads(const char* env, int lo, int hi, int def) {  // tuning.cc:14-32
-  int64_t nt = envInt(env, -2);
+static int clampNthreads(int nt, int lo, int hi, int def) {  // tuning.cc:14-32
   if (nt > 0) {
     if (nt % kRefWarp != 0) return hi;
     if (nt > hi) return hi;
     if (nt < lo) return lo;
-    return (int)nt;
+    return nt;
   }
   return def;
 }
 
-int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, Plan* p) {
+int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, const Knobs& k,
+             Plan* p) {
   const Algorithm& a = algos[algoIndex];
   *p = Plan();
   p->algoIndex = algoIndex;
   p->proto = protoOverride >= 0 ? protoOverride : a.proto;
   argsCheck(c, &p->count, &p->dtype, &p->nBytes);
   int nt;
-  if (p->proto == kProtoSimple) nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512);
-  else if (p->proto == kProtoLL) nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512);
-  else nt = getNthreads("NCCL_LL128_NTHREADS", 640 / 4, 640, 640);
+  if (p->proto == kProtoSimple) nt = clampNthreads(k.nthreads, 2 * kRefWarp, 512, 512);
+  else if (p->proto == kProtoLL) nt = clampNthreads(k.nthreads, 2 * kRefWarp, 512, 512);
+  else nt = clampNthreads(k.ll128Nthreads, 640 / 4, 640, 640);
   if (a.nThreads > 0) nt = std::min(nt, a.nThreads);
   if (p->proto == kProtoSimple) nt += kRefWarp;  // extra sync warp (enqueue.cc:516-517)
   p->refNthreads = nt;
-  int64_t bs[3] = {envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16),
-                   envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8), envInt("NCCL_BUFFSIZE", 1 << 22)};
+  const int64_t* bs = k.buffSizes;
   int64_t stepSize = bs[p->proto] / kFifoSteps;
   int64_t chunkSteps = p->proto == kProtoSimple ? kChunkSteps : 1;
   int64_t chunkSize = stepSize * chunkSteps;
@@ -184,7 +198,7 @@ int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverri
   return 0;
 }
 
-int makeRingPlan(const CallDesc& c, Plan* p) {
+int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   *p = Plan();
   p->algoIndex = -1;
   if (!(c.redop == 0 || c.redop == 1 || c.redop == 2 || c.redop == 3)) return 5;
@@ -194,21 +208,20 @@ int makeRingPlan(const CallDesc& c, Plan* p) {
   else return 5;
   argsCheck(c, &p->count, &p->dtype, &p->nBytes);   // AllGather: bytes, int8 (argcheck.cc:44-51)
   const int ts = refTypeSize(p->dtype);
-  const bool llOk = protoEnabled(kProtoLL), simpleOk = protoEnabled(kProtoSimple);
+  const bool llOk = k.protoOn[kProtoLL], simpleOk = k.protoOn[kProtoSimple];
   if (!llOk && !simpleOk) return 5;
   p->proto = (llOk && (p->nBytes <= (512 << 10) || !simpleOk)) ? kProtoLL : kProtoSimple;
-  const int64_t forced = envInt("MSCCL_AMD_RING_CHANNELS", 0);
+  const int64_t forced = k.ringChannels;
   int64_t ch = forced > 0 ? forced : std::max<int64_t>(1, p->nBytes >> 18);
   p->ringChannels = (int)std::max<int64_t>(1, std::min<int64_t>(kRingChannels, ch));
-  const int64_t bs[3] = {envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16),
-                         envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8), envInt("NCCL_BUFFSIZE", 1 << 22)};
+  const int64_t* bs = k.buffSizes;
   int nt;
   if (p->proto == kProtoLL) {
-    nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512);
+    nt = clampNthreads(k.nthreads, 2 * kRefWarp, 512, 512);
     p->chunkSize = bs[0] / kFifoSteps / 2 / ts;             // calcBytePerStep (primitives.h:49-51)
     p->minChunk = (int64_t)nt * 8 / ts;                      // all_reduce.h:30-31
   } else {
-    nt = getNthreads("NCCL_NTHREADS", 2 * kRefWarp, 512, 512) + kRefWarp;  // enqueue.cc:516-517
+    nt = clampNthreads(k.nthreads, 2 * kRefWarp, 512, 512) + kRefWarp;  // enqueue.cc:516-517
     p->chunkSize = bs[2] / kFifoSteps / ts * kChunkSteps;   // x ALLREDUCE/REDUCESCATTER/ALLGATHER_CHUNKSTEPS
     p->minChunk = (int64_t)(nt - kRefWarp) * 8 / ts;         // all_reduce.h:45 rounding unit
   }

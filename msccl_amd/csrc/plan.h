@@ -47,25 +47,43 @@ struct Plan {
   int64_t ringLastChunk = 0;  // LL ReduceScatter / AllGather lastChunkSize (elements)
 };
 
+// Every environment knob the per-call planning reads, captured once at communicator init
+// (NCCL_PARAM caches its getenv the same way, include/param.h:99-108).  All ranks must plan
+// identical launch geometry, so init also checks that every rank captured the same values
+// (init.cc: the SplitRecord allgather).  Plain data: compared with memcmp.
+struct Knobs {
+  int32_t mscclOn;           // NCCL_ALGO enables MSCCL (tuning.cc:186,217; on unless excluded here)
+  int32_t protoOn[3];        // NCCL_PROTO gates per protocol (tuning.cc:188-197)
+  int32_t nthreads;          // NCCL_NTHREADS (-2 = unset, tuning.cc:12)
+  int32_t ll128Nthreads;     // NCCL_LL128_NTHREADS (tuning.cc:13)
+  int64_t buffSizes[3];      // NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE / NCCL_BUFFSIZE (init.cc:455-472)
+  int32_t ringChannels;      // MSCCL_AMD_RING_CHANNELS (0 = auto)
+  int32_t split;             // MSCCL_AMD_SPLIT (0 = auto)
+  int32_t targetWgs;         // MSCCL_AMD_TARGET_WGS
+  int32_t merge;             // MSCCL_AMD_MERGE (0 = as many as fit)
+  int32_t ringFallback;      // MSCCL_AMD_RING_FALLBACK
+  int32_t ll128Remote;       // MSCCL_AMD_LL128_REMOTE: allow LL128 towards peers on other GPUs
+  static Knobs fromEnv();
+};
+
 int refTypeSize(int dtype);
 bool inPlaceOf(int coll, const void* send, const void* recv, size_t count, int dtype, int rank);
 // Returns the selected algorithm index or -1 (the reference falls back to ring/tree there).
-int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c);
+int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c,
+               const Knobs& k);
 // Fills *p; returns an ncclResult_t code.
-int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, Plan* p);
+int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, const Knobs& k,
+             Plan* p);
 // Workgroups per XML thread block for an algorithm whose largest rank program has maxBlocks
 // thread blocks when coResident ranks share a GPU: the largest power of two <= kMaxSplit that
 // keeps the GPU's workgroups within MSCCL_AMD_TARGET_WGS (default 256 = one per CU).
 // MSCCL_AMD_SPLIT forces a value.  Every rank must compute the same value.
-int chooseSplit(int maxBlocks, int coResident);
+int chooseSplit(int maxBlocks, int coResident, const Knobs& k);
 // The reference's fallback when no MSCCL algorithm matches (enqueue.cc:461-476): a ring
 // AllReduce / ReduceScatter / AllGather (collectives/device/all_reduce.h:14-100,
 // reduce_scatter.h:13-67, all_gather.h:13-78).  Fills *p (algoIndex -1, ringColl set) and returns
 // 0, or returns ncclInvalidUsage when the collective / op has no ring (AllToAll, custom, Avg).
 // Channels, protocol and thread count are this build's choice (oracle/ring.py: ring_params).
-int makeRingPlan(const CallDesc& c, Plan* p);
-// NCCL_ALGO / NCCL_PROTO gates
-bool mscclEnabled();
-bool protoEnabled(int proto);
+int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p);
 
 }  // namespace msccl

@@ -27,9 +27,14 @@ size_t alignUp(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 ncclResult_t transportPlan(ncclComm* comm) {
   const int n = comm->nRanks;
-  comm->buffSizes[kProtoLL] = (int)envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16);
-  comm->buffSizes[kProtoLL128] = (int)envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8);
-  comm->buffSizes[kProtoSimple] = (int)envInt("NCCL_BUFFSIZE", 1 << 22);
+  for (int p = 0; p < 3; p++) {
+    // a FIFO slot must stay far below the 2 GiB reach of a buffer descriptor (interpreter.h)
+    if (comm->knobs.buffSizes[p] <= 0 || comm->knobs.buffSizes[p] > (1ll << 30)) {
+      WARN("MSCCL: FIFO buffer size %lld (protocol %d) outside (0, 1 GiB]", (long long)comm->knobs.buffSizes[p], p);
+      return ncclInvalidArgument;
+    }
+    comm->buffSizes[p] = (int)comm->knobs.buffSizes[p];
+  }
   comm->llSlotLines = comm->buffSizes[kProtoLL] / kFifoSteps / 16;
   comm->simpleSlotBytes = comm->buffSizes[kProtoSimple] / kFifoSteps / 16 * 16;
   if (comm->llSlotLines < 128 || comm->simpleSlotBytes < 4096) {
@@ -272,7 +277,7 @@ ncclResult_t ringUpload(ncclComm* comm) {
 // Pack every algorithm's per-tb programs and upload them (replaces the 29 MB
 // mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 // Longest run of chunks a thread block sends before it next receives (merge bound, devcomm.h).
-static int sendRunOf(const Algorithm& a) {
+int algoSendRunOf(const Algorithm& a) {
   int best = 0;
   for (int b = 0; b < a.nBlocks; b++) {
     int run = 0;
@@ -288,8 +293,6 @@ static int sendRunOf(const Algorithm& a) {
 
 ncclResult_t algoUpload(ncclComm* comm) {
   comm->devAlgos.clear();
-  comm->algoSendRun.clear();
-  for (auto& a : comm->algos) comm->algoSendRun.push_back(sendRunOf(a));
   for (auto& a : comm->algos) {
     DevAlgoHost d;
     d.nBlocks = a.nBlocks;

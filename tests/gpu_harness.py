@@ -211,3 +211,118 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
         if iters > 1 and coll == L.ALLREDUCE and in_place:
             o_in = res
     return gpu, [np.asarray(r) for r in res], rp
+
+
+# ---------------------------------------------------------------------------------------------
+# Mismatch reports and numeric bounds shared by the parity tests
+
+
+def describe_mismatch(got: np.ndarray, want: np.ndarray, chunk_elems: Optional[int] = None, limit: int = 6) -> str:
+    """Where two arrays differ: count, first runs of differing elements (with their MSCCL chunk
+    when chunk_elems is given) and whether the bad values are zeros or equal to other places of
+    the expected array (misplaced data) — enough to localise a FIFO or offset fault from one
+    failure record."""
+    g = np.ascontiguousarray(got).view(np.uint8).reshape(len(got), -1)
+    w = np.ascontiguousarray(want).view(np.uint8).reshape(len(want), -1)
+    bad = np.flatnonzero((g != w).any(axis=1))
+    if len(bad) == 0:
+        return "identical"
+    runs = np.split(bad, np.flatnonzero(np.diff(bad) != 1) + 1)
+    out = ["%d of %d elements differ in %d runs" % (len(bad), len(got), len(runs))]
+    for run in runs[:limit]:
+        a, b = int(run[0]), int(run[-1]) + 1
+        seg = g[a:b]
+        what = "zeros" if not seg.any() else "values"
+        where = ""
+        if chunk_elems:
+            where = " (chunk %d +%d)" % (a // chunk_elems, a % chunk_elems)
+        out.append("  [%d, %d)%s: %s, got %s want %s" % (a, b, where, what, got[a:min(b, a + 3)], want[a:min(b, a + 3)]))
+    return "\n".join(out)
+
+
+def sum_error_ok(result: np.ndarray, inputs: List[np.ndarray], dt: int) -> tuple:
+    """Checks |result - exact sum| <= (n-1) * u * sum|x_i| elementwise (the classical bound for
+    any association order of n-1 roundings at unit roundoff u), and returns (ok, worst ratio)."""
+    n = len(inputs)
+    u = {6: 2.0 ** -11, 7: 2.0 ** -24, 9: 2.0 ** -8, 8: 2.0 ** -53}[dt]
+    xs = [N.to_float64(dt, x) for x in inputs]
+    exact = np.sum(xs, axis=0)
+    mag = np.sum(np.abs(xs), axis=0)
+    err = np.abs(N.to_float64(dt, result) - exact)
+    bound = (n - 1) * u * mag + 1e-30
+    ratio = float(np.max(err / bound)) if len(err) else 0.0
+    return ratio <= 1.0, ratio
+
+
+class CoResident:
+    """n ranks on cuda:0 created by one ncclCommInitAll with several XML schedules registered
+    (MSCCL_XML_FILES, as a user registers size tiers).  run() issues one grouped collective;
+    oracle() computes what the reference would produce for the same call: the schedule the
+    reference's selection picks (oracle/plan.py), or its ring fallback (oracle/ring.py)."""
+
+    def __init__(self, n: int, xml_texts: List[str], tmpdir: str = "/tmp"):
+        self.n = n
+        self.paths = []
+        for i, x in enumerate(xml_texts):
+            p = os.path.join(tmpdir, "msccl_cores_%d_%d_%d.xml" % (os.getpid(), i, abs(hash(x)) % 100000))
+            with open(p, "w") as f:
+                f.write(x)
+            self.paths.append(p)
+        os.environ["MSCCL_XML_FILES"] = ":".join(self.paths)
+        self.algos = [[L.parse_xml(x, r, n) for x in xml_texts] for r in range(n)]
+        self.comms = M.Comm.init_all([0] * n)
+
+    def close(self):
+        for c in self.comms:
+            c.destroy()
+        self.comms = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def run(self, coll: int, count: int, dt: int, op: int, sends, recvs, stream: int = 0):
+        import torch
+        with M.group():
+            for r, c in enumerate(self.comms):
+                if coll == L.ALLREDUCE:
+                    c.all_reduce(sends[r], recvs[r], count, dt, op, stream)
+                elif coll == L.REDUCE_SCATTER:
+                    c.reduce_scatter(sends[r], recvs[r], count, dt, op, stream)
+                else:
+                    c.all_gather(sends[r], recvs[r], count, dt, stream)
+        torch.cuda.synchronize()
+        for c in self.comms:
+            if c.async_error() != 0:
+                raise M.NcclError(c.async_error(), "kernel (async error)")
+
+    def oracle(self, coll: int, count: int, dt: int, op: int, ins: List[np.ndarray], in_place: bool):
+        """Expected outputs (interpreter element type) and the schedule used ('ring' or index)."""
+        call = P.Call(coll, count, dt, op, self.n, 0, in_place)
+        idx = P.select(self.algos[0], call)
+        ts = N.type_size(dt)
+        out_n = count if coll != L.ALLGATHER else count * self.n
+        if idx is None:
+            from oracle import ring as R
+            o_in = [x.copy() for x in ins]
+            o_out = [None] * self.n if in_place and coll == L.ALLREDUCE else \
+                [np.zeros(out_n, N.storage(dt)) for _ in range(self.n)]
+            res, _ = R.run(coll, count, dt, op, o_in, o_out, in_place)
+            return [np.asarray(r) for r in res], "ring"
+        algos = [a[idx] for a in self.algos]
+        plan = P.make_plan(self.algos[0], call, idx)
+        o_in = [x.copy() for x in ins]
+        if coll == L.ALLGATHER:
+            o_in = [x.view(np.int8) for x in o_in]
+            o_out = [np.zeros(out_n * ts, np.int8) for _ in range(self.n)]
+        elif in_place:
+            o_out = [None] * self.n
+        else:
+            o_out = [np.zeros(out_n, N.storage(dt)) for _ in range(self.n)]
+        res, _ = S.run(algos, plan, o_in, o_out, coll, in_place)
+        res = [np.asarray(r) for r in res]
+        if coll == L.ALLGATHER:
+            res = [r.view(N.storage(dt)) for r in res]
+        return res, idx

@@ -73,8 +73,12 @@ def test_rccl_alltoall_schedules(name):
     count = max(ncpl, (a.minBytes // (ts * n) // ncpl + 1) * ncpl)   # nBytes = count*ts*n >= minBytes
     assert a.minBytes <= count * ts * n < a.maxBytes, (count, a.minBytes, a.maxBytes)
     ins, gpu, ora = run_xml(xml, n, L.ALLTOALL, count, dt)
+    from tests.gpu_harness import describe_mismatch
+    chunk = count * n // ncpl   # elements (fp32) of one MSCCL chunk
     for r in range(n):
-        assert np.array_equal(gpu[r].view(np.uint8), ora[r].view(np.uint8)), r
+        assert np.array_equal(gpu[r].view(np.uint8), ora[r].view(np.uint8)), \
+            "rank %d (chunks of %d floats, block q = chunks [q*%d, (q+1)*%d)):\n%s" % (
+                r, chunk, ncpl // n, ncpl // n, describe_mismatch(gpu[r], ora[r], chunk))
         # the collective's definition: block p of rank r's output is block r of rank p's input
         for q in range(n):
             assert np.array_equal(gpu[r][q * count:(q + 1) * count], ins[q][r * count:(r + 1) * count]), (r, q)
