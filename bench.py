@@ -57,9 +57,10 @@ def parse():
     return ap.parse_args()
 
 
-def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int):
-    """Algorithmic HBM bytes and wire bytes of one launch for one rank (whole schedule)."""
-    f = {0: 2.0, 1: 4.0 / 3.0}.get(proto, 1.0)  # LL: 8 B data per 16-B line; CDNA4 LL128: 12 B
+def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only: bool = False):
+    """Algorithmic HBM bytes and wire bytes of one launch for one rank (whole schedule).
+    payload_only counts FIFO traffic at its payload size (LL flags / LL128 flag words excluded)."""
+    f = 1.0 if payload_only else {0: 2.0, 1: 4.0 / 3.0}.get(proto, 1.0)  # LL: 8 B data per 16-B line
     hbm = wire = 0
     for tb in algo["tbs"]:
         for t in tb["transfers"]:
@@ -93,16 +94,20 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
     all-pairs, 1 instance below 64 KiB, inst_large above."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
-        # "O" = rank-ordered one-shot
+        # "O" = rank-ordered one-shot, "p" = 2-rank one-hop exchange (s, rrc), "r" = ring with
+        # `instances` channels (for 2 ranks the fused all-pairs exchange s, rrcs, r)
         spec = []
         for t in tiers_arg.split(","):
             f = t.split(":")
             spec.append((int(f[0]), int(f[1]), int(f[2])) + ((f[3],) if len(f) > 3 else ()))
     elif n <= 2:
-        # below 16 MiB the one-shot schedule (s, r, re: 3 transfers on the critical path instead
-        # of 7) wins: 128 B 18.4 -> 13.3 us, 4 MiB 27.3 -> 24.2 us; from 16 MiB on the two-phase
-        # all-pairs moves fewer HBM bytes (7.5 S vs 9 S per rank) and wins (DESIGN.md §4)
-        spec = [(0, 4 << 10, 1, "o"), (4 << 10, 16 << 20, 16, "o"), (16 << 20, (1 << 30) + 1, inst_large)]
+        # Two ranks: the all-pairs exchange fused into one hop per thread block (s, rrc:
+        # xmlgen.allreduce_pair_oneshot): no scratch, no cross-tb dependency, 7 S HBM bytes per
+        # rank against the two-phase schedule's 7.5 S.  One instance below 4 KiB (latency), 16
+        # above; measured over the whole sweep against the two-phase all-pairs and ring forms
+        # (profiles/r02_tier_sweep2.txt): 128 B 14.8 -> 11.8 us, 1 MiB 50 -> 78 GB/s,
+        # 32 MiB 398 -> 450 GB/s
+        spec = [(0, 4 << 10, 1, "p"), (4 << 10, (1 << 30) + 1, inst_large, "p")]
     else:
         # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 16 KiB: 8 ranks
         # on one MI355X, fp16, 128 B 23.2 -> 19.5 us (profiles/r01_tier_sweep8.txt); it moves
@@ -115,6 +120,10 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         if kind in ("o", "O"):
             x = xmlgen.allreduce_oneshot(n, inst, proto, lo, hi, name="oneshot_t%d_i%d" % (k, inst),
                                          ordered=kind == "O")
+        elif kind == "p":
+            x = xmlgen.allreduce_pair_oneshot(inst, proto, True, lo, hi, name="pair_t%d_i%d" % (k, inst))
+        elif kind == "r":
+            x = xmlgen.allreduce_ring(n, inst, proto, True, lo, hi, name="ring_t%d_i%d" % (k, inst))
         else:
             x = xmlgen.allreduce_allpairs(n, inst, proto, True, lo, hi, name="allpairs_t%d_i%d" % (k, inst))
         pth = os.path.join(tmp, "bench_ap%d_%s_t%d_i%d_%s_%d.xml" % (n, proto, k, inst, kind, os.getpid()))
@@ -232,6 +241,20 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
     stream = torch.cuda.Stream(dev)
     nloc = len(comms)
     try:
+        ranks = [rank] if multi else list(range(n))
+        tdt = {M.BFLOAT16: torch.bfloat16, M.FLOAT32: torch.float32}[dt]
+
+        def pattern(r, cnt):
+            j = torch.arange(cnt, device=dev, dtype=torch.int64)
+            return ((j * 5 + r * 3 + (j >> 7)) % 9 - 4).to(tdt)
+
+        def agree(good):
+            if multi:
+                g = torch.tensor([1 if good else 0], dtype=torch.int32)
+                torch.distributed.all_reduce(g, op=torch.distributed.ReduceOp.MIN)
+                good = bool(g.item())
+            return good
+
         if cfg in ("C4", "FB"):
             cnt = S // ts
             bufs = [torch.zeros((S + 1) // 2, dtype=torch.int16, device=dev) for _ in range(nloc)]
@@ -240,6 +263,15 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 with M.group():
                     for c, b in zip(comms, bufs):
                         c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+
+            def check():
+                for r, b in zip(ranks, bufs):
+                    b.view(torch.uint8)[:S].view(tdt).copy_(pattern(r, cnt))
+                want = sum(pattern(r, cnt).float() for r in range(n)).to(tdt)
+                torch.cuda.synchronize()
+                step()
+                torch.cuda.synchronize()
+                return agree(all(torch.equal(b.view(torch.uint8)[:S].view(tdt), want) for b in bufs))
             phases = {"allreduce": (step, S * 2 * (n - 1) / n)}
         else:
             rc = S // ts // n
@@ -256,6 +288,17 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 with M.group():
                     for c, m, o in zip(comms, mids, outs):
                         c.all_gather(m.data_ptr(), o.data_ptr(), rc, dt, stream.cuda_stream)
+
+            def check():
+                for r, i in zip(ranks, ins):
+                    i.copy_(pattern(r, S // 4))
+                full = sum(pattern(r, S // 4).float() for r in range(n))
+                torch.cuda.synchronize()
+                rs()
+                ag()
+                torch.cuda.synchronize()
+                good = all(torch.equal(m, full[r * rc:(r + 1) * rc]) for r, m in zip(ranks, mids))
+                return agree(good and all(torch.equal(o, full) for o in outs))
             phases = {"reduce_scatter": (rs, S * (n - 1) / n), "all_gather": (ag, S * (n - 1) / n)}
         res = {}
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -286,6 +329,7 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
             res[name] = {"ms": round(t * 1e3, 4), "kernel_ms": round(ev_ms, 4),
                          "busbw": round(busbytes / t / 1e9, 3), "steps": k}
             note("%s %.3f ms, busbw %.1f GB/s" % (name, t * 1e3, busbytes / t / 1e9))
+        res["verified"] = check()
         res["bytes"] = S
         res["dtype"] = {M.BFLOAT16: "bf16", M.FLOAT32: "f32"}[dt]
         res["ranks"] = n
@@ -358,12 +402,37 @@ def main():
             for c, b in zip(comms, bufs):
                 c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
 
+    def pattern(r, cnt, dev):
+        # exact small integers (|x| <= 4): every partial sum of up to 8 ranks is exact in every
+        # dtype, so any association order must give exactly sum_r pattern(r)
+        j = torch.arange(cnt, device=dev, dtype=torch.int64)
+        return ((j * 7 + r * 3 + (j >> 5)) % 9 - 4).to(torch.float32)
+
+    def verify(nbytes):
+        """One step on exact-integer inputs after the timed steps: the result on every local rank
+        must be the exact sum over all ranks (the timed kernel provably did the work)."""
+        cnt = nbytes // ts
+        tdt = {M.FLOAT32: torch.float32, M.FLOAT16: torch.float16, M.BFLOAT16: torch.bfloat16}[dt]
+        for r, b in zip(my_ranks, bufs):
+            b.view(tdt)[:cnt].copy_(pattern(r, cnt, b.device).to(tdt))
+        want = sum(pattern(r, cnt, bufs[0].device) for r in range(n)).to(tdt)
+        torch.cuda.synchronize()   # the refill runs on torch's stream, the collective on `stream`
+        one_step(nbytes)
+        torch.cuda.synchronize()
+        good = all(torch.equal(b.view(tdt)[:cnt], want) for b in bufs)
+        if multi:
+            g = torch.tensor([1 if good else 0], dtype=torch.int32)
+            torch.distributed.all_reduce(g, op=torch.distributed.ReduceOp.MIN)
+            good = bool(g.item())
+        return good
+
     results = []
+    verified = []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for nbytes in sizes:
         cnt = nbytes // ts
         tier = tier_of(tiers, nbytes)
-        ncpl = tier[2] * (n * n if tier[4] == "a" else 1)  # one-shot: instances
+        ncpl = algos[tier[3]]["nchunksperloop"]
         if cnt % ncpl:
             continue
         for _ in range(a.warmup):
@@ -404,7 +473,11 @@ def main():
         algo = algos[tier[3]]
         size_per = cnt // ncpl
         hbm, wire = schedule_bytes(algo, size_per, ts, proto_id)
+        payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True)
+        ok = verify(nbytes)
+        verified.append(ok)
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
+                        "payload_bytes_per_rank": payload, "verified": ok,
                          "algbw": round(algbw, 3), "busbw": round(bus, 3),
                          "hbm_bytes_per_rank": hbm, "wire_bytes_per_rank": wire})
         if not a.quiet and rank == 0:
@@ -415,8 +488,14 @@ def main():
     ranks_on_gpu = 1 if multi else n
     kernel_s = head["kernel_ms"] / 1e3
     achieved = head["hbm_bytes_per_rank"] * ranks_on_gpu / kernel_s / 1e9
+    payload_rate = head["payload_bytes_per_rank"] * ranks_on_gpu / kernel_s / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "payload_achieved": round(payload_rate, 2),
+            "note": ("achieved counts the protocol's FIFO bytes (LL: 16-B line per 8-B payload); "
+                     "payload_achieved counts them at payload size.  The launch's buffers (%d MiB, plus "
+                     "FIFO slots) fit the 256 MB MALL, whose hits FETCH_SIZE counts: traffic is "
+                     "memory-side bytes, not HBM-array bytes" % (head["bytes"] * ranks_on_gpu >> 20)),
             "kernel": "mscclKernel<%s,Sum,%s>" % (dtname, a.proto),
             "algorithmic_bytes_per_launch": head["hbm_bytes_per_rank"] * ranks_on_gpu,
             "kernel_ms": head["kernel_ms"]}
@@ -454,17 +533,21 @@ def main():
         "config": {"workload": workload,
                    "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
-                   "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot", "O": "oneshot-ordered"}[t[4]]] for t in tiers],
+                   "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot", "O": "oneshot-ordered",
+                                                 "p": "pair-oneshot", "r": "ring"}[t[4]]] for t in tiers],
                    "launch": "hipgraph" if a.graph else "eager",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
+        "verified": bool(verified) and all(verified),
+        "verification": "after each size's timed steps, one step on exact-integer inputs on every rank "
+                        "must equal the exact sum over ranks",
         # `value` is the metric as BASELINE.json and nccl-tests define it (bus bandwidth seen by
         # each rank); the whole job moves n_ranks times that
         "aggregate": {"ranks": n, "busbw_sum_gbs": round(head["busbw"] * n, 3),
                       "algbw_sum_gbs": round(head["bytes"] / (head["ms"] / 1e3) / 1e9 * n, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw")} for r in results],
+        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw", "verified")} for r in results],
     }
     if e2e:
         out["e2e"] = e2e

@@ -20,26 +20,31 @@ class Bootstrap;
 
 constexpr uint64_t kCommMagic = 0x6d7363636c616d64ull;  // "msccl amd"
 
-// Connection key: (channel, peer)
+// Connection key: (group, channel, peer); group = algorithm index, or kRingGroup for the ring
+// fallback's channels.  Every group owns its connections (transport.cc).
+constexpr int kRingGroup = kMaxAlgos;
 struct ConnKey {
-  int chan, peer;
-  bool operator<(const ConnKey& o) const { return chan != o.chan ? chan < o.chan : peer < o.peer; }
-  bool operator==(const ConnKey& o) const { return chan == o.chan && peer == o.peer; }
+  int group, chan, peer;
 };
 
-// Per-rank transport table exchanged during init: for every (channel, peer) the offsets,
+// Per-rank transport table exchanged during init: for every (group, channel, peer) the offsets,
 // inside this rank's transport arena, of the receive FIFOs / tail word (this rank receiving
 // from peer) and of the head word (this rank sending to peer).  -1 = no connection.
-// Sub-connection k (0 <= k < maxSplit) of a key sits at base + k * stride.
+// Sub-connection k of a key sits at base + k * stride.
 struct PeerOffsets {
   int64_t recvLL, recvSimple, recvTail, sendHead;
   int64_t llStride, simpleStride, wordStride, pad;
 };
 
+// One algorithm (or ring program) on the device: fixed-stride thread-block images and the
+// slot-indexed connection records (entry tb * connSplit + sub) of its thread blocks.
 struct DevAlgoHost {
-  DevTbHeader* dTbs = nullptr;
-  char* dBlob = nullptr;
+  char* dImages = nullptr;
+  int tbStride = 0;
   int nBlocks = 0;
+  DevSendConn* dSend = nullptr;
+  DevRecvConn* dRecv = nullptr;
+  int connSplit = 1;
 };
 
 struct ncclCommImpl;
@@ -64,14 +69,13 @@ struct ncclComm {
 
   // transport
   std::vector<msccl::ConnKey> sendKeys, recvKeys;
-  std::vector<uint8_t> sendProtoMask, recvProtoMask;  // bit p = protocol p used
   char* arena = nullptr;
   size_t arenaSize = 0;
-  std::vector<msccl::PeerOffsets> table;              // [kTableChannels * nRanks] own table
+  std::vector<msccl::PeerOffsets> table;              // [(kMaxAlgos + 1) * kMaxChannels * nRanks] own table
   std::vector<char*> peerArena;                        // per rank: mapped arena base
   std::vector<bool> peerArenaIpc;                      // opened through hipIpcOpenMemHandle
-  msccl::DevSendConn* dSend = nullptr;
-  msccl::DevRecvConn* dRecv = nullptr;
+  msccl::DevSendConn* ringSend = nullptr;              // ring fallback connections [kRingChannels]
+  msccl::DevRecvConn* ringRecv = nullptr;
   int llSlotLines = 0, simpleSlotBytes = 0;
   int buffSizes[3] = {0, 0, 0};
 
@@ -89,7 +93,9 @@ struct ncclComm {
   uint32_t* hostErr = nullptr;     // mapped
   uint32_t* devAbort = nullptr;
   uint32_t* devErr = nullptr;
-  double timeoutSec = 60.0;
+  double timeoutSec = 0.0;         // MSCCL_AMD_TIMEOUT_SEC: bound on a single device wait (0 = none)
+  uint64_t timeoutTicks = 0;       // the same in s_memrealtime ticks (100 MHz)
+  uint32_t llFlagMask = 0xffffffffu, llCleanMask = 0x7ffffff8u;  // MSCCL_AMD_TEST_LL_CLEANUP
   ncclResult_t asyncError = ncclSuccess;
 
   // rendezvous
@@ -115,6 +121,7 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier);
 bool commValid(const ncclComm* comm);
 
 // transport.cc
+size_t tableIndex(int group, int chan, int peer, int nRanks);
 ncclResult_t transportPlan(ncclComm* comm);                 // keys, arena layout, allocation, own table
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
                               const std::vector<char*>& peerBases, const std::vector<int>& peerRemote);

@@ -62,12 +62,17 @@ struct alignas(16) DevTransfer {
 };
 static_assert(sizeof(DevTransfer) == 16, "DevTransfer must be 16 bytes");
 
+// First 16 B of a thread-block image.  Image = [DevTbHeader][nsteps DevTransfer][ndeps int16
+// dependency tb][ndeps int16 dependency step][nreds int16 reduction source offset], padded to
+// 16 B; a group's images have one stride (RankWork::tbStride), so workgroup b finds image b
+// without first reading a table (one memory round trip in the kernel prologue).
 struct alignas(16) DevTbHeader {
-  int16_t sendConn, recvConn;   // index into DevComm::send / ::recv, -1 if none
+  int16_t hasSend, hasRecv;     // the tb's connection records (RankWork::send / ::recv) are in use
   uint16_t nsteps, ndeps;
   uint16_t nreds, pad;
-  uint32_t blobOffset;          // bytes: [nsteps DevTransfer][ndeps int16 bid][ndeps int16 step][nreds int16 off]
+  uint32_t reserved;
 };
+constexpr int kMaxImage16 = 1 + 256 + (3 * 256 * 2 + 15) / 16;  // largest image in 16-B units
 static_assert(sizeof(DevTbHeader) == 16, "DevTbHeader must be 16 bytes");
 
 struct DevSendConn {
@@ -92,11 +97,11 @@ struct DevRecvConn {
   uint64_t tailSeen;            // last Simple tail value read (data known present below it)
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
+  int32_t pad[2];
 };
+static_assert(sizeof(DevSendConn) == 64 && sizeof(DevRecvConn) == 64, "connection records are four 16-B units");
 
 struct DevComm {
-  DevSendConn* send;
-  DevRecvConn* recv;
   uint64_t* flags;              // [kFlagSlots * kFlagStride]
   volatile uint32_t* abortFlag; // host-mapped
   uint32_t* errWord;            // host-mapped: 0 ok, else error code (1 timeout, 2 bad program)
@@ -143,8 +148,9 @@ struct RankWork {
   uint64_t* epochs;
   int32_t maxSplit;
   int32_t pad0;
-  const DevTbHeader* tbs;
-  const char* blob;
+  const char* images;           // thread-block images, tbStride bytes each
+  int32_t tbStride;
+  int32_t connSplit;            // connection record of (tb, sub): send / recv [tb * connSplit + sub]
   int64_t sizePerChunk;         // sizePerMscclChunk = count*sizeMultiplier/nchunksPerLoop (elements)
   int64_t chunkSize;            // interpreter chunkSize (elements)
   int64_t minChunk;             // LL: nthreads*8/sizeof(T); Simple: rounding unit (nthreads-32)*8/sizeof(T)
@@ -162,6 +168,12 @@ struct RankWork {
   int16_t ringRanks;
   int64_t ringSize;             // elements of one rank's block (args->count)
   int64_t ringLastChunk;        // LL ReduceScatter / AllGather lastChunkSize (enqueue.cc:653-658)
+  // copies of per-communicator constants (kernel arguments: no dependent DevComm load)
+  uint64_t timeoutTicks;
+  uint32_t llFlagMask, llCleanMask;
+  struct TraceEvent* trace;
+  int32_t traceEvents;
+  int32_t pad1;
 };
 
 struct LaunchArgs {

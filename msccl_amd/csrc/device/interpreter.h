@@ -32,14 +32,10 @@ enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy
 enum : int { pLL = 0, pLL128 = 1, pSimple = 2 };
 
 struct alignas(16) BlockShared {
-  DevTransfer tr[256];
-  int16_t depBid[256];
-  int16_t depStep[256];
-  int16_t red[256];
-  DevSendConn sconn;  // this workgroup's connections, copied once per launch (no global
-  DevRecvConn rconn;  // load of connection metadata on the primitives' critical path)
-  uint64_t step[2];
-  uint64_t seen[2];  // send head / recv tail last observed
+  u32x4 img[kMaxImage16];  // this workgroup's thread-block image (devcomm.h: DevTbHeader)
+  DevSendConn sconn;       // its connection records, copied once per launch (no global load of
+  DevRecvConn rconn;       // connection metadata on the primitives' critical path)
+  uint64_t seen[2];        // send head / recv tail last observed
   uint64_t epoch;
   uint32_t aborted;
 };
@@ -85,6 +81,10 @@ struct Interp {
   DevComm* comm;
   DevSendConn* sc;   // LDS copies (read-only in the primitives)
   DevRecvConn* rc;
+  const DevTransfer* tr;  // the program in LDS (BlockShared::img)
+  const int16_t* depBid;
+  const int16_t* depStep;
+  const int16_t* red;
   DevSendConn* scG;  // global connection state (step counters written back at the end)
   DevRecvConn* rcG;
   uint64_t sendStep, recvStep;
@@ -728,51 +728,50 @@ struct Interp {
     comm = w.comm;
     refNthreads = w.refNthreads;
     t0 = __builtin_amdgcn_s_memrealtime();
-    timeoutTicks = uni(comm->timeoutTicks);
-    llFlagMask = uni(comm->llFlagMask);
-    llCleanMask = uni(comm->llCleanMask);
+    timeoutTicks = w.timeoutTicks;
+    llFlagMask = w.llFlagMask;
+    llCleanMask = w.llCleanMask;
     const int split = w.split;
     const int maxSplit = w.maxSplit;
-    const int slot = bid * maxSplit + sub;  // flag / epoch / trace slot of this workgroup
+    const int slot = bid * maxSplit + sub;        // flag / epoch / trace slot of this workgroup
+    const int cslot = bid * w.connSplit + sub;    // its connection records
+    // Prologue: one memory round trip.  The image (header + program), both connection records
+    // and the launch epoch sit at addresses known from the block index, so all of them are in
+    // flight together: image by every lane with a 16-B unit, records by lanes 0-3 / 64-67 (other
+    // waves), the epoch by a lane of a third wave.
+    {
+      const u32x4* gimg = (const u32x4*)(w.images + (size_t)bid * w.tbStride);
+      const int nU = w.tbStride >> 4;
+      for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
+      if (tid < 4) ((u32x4*)&sh->sconn)[tid] = ((const u32x4*)(w.send + cslot))[tid];
+      if (tid >= 64 && tid < 68) ((u32x4*)&sh->rconn)[tid - 64] = ((const u32x4*)(w.recv + cslot))[tid - 64];
+      if (tid == 128) {
+        sh->aborted = 0;
+        sh->epoch = atomicLoadAgent(w.epochs + slot);
+      }
+    }
+    __syncthreads();
     DevTbHeader hd;
     {
-      u32x4 raw = *(const u32x4*)&w.tbs[bid];
+      u32x4 raw = sh->img[0];
       raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
       __builtin_memcpy(&hd, &raw, sizeof(hd));
     }
-    // stage the tb program in LDS
-    const DevTransfer* gtr = (const DevTransfer*)(w.blob + hd.blobOffset);
-    const int16_t* gdep = (const int16_t*)(gtr + hd.nsteps);
-    for (int i = tid; i < hd.nsteps; i += kNT) sh->tr[i] = gtr[i];
-    for (int i = tid; i < hd.ndeps; i += kNT) {
-      sh->depBid[i] = gdep[i];
-      sh->depStep[i] = gdep[hd.ndeps + i];
-    }
-    for (int i = tid; i < hd.nreds; i += kNT) sh->red[i] = gdep[2 * hd.ndeps + i];
-    scG = hd.sendConn >= 0 ? w.send + (size_t)hd.sendConn * maxSplit + sub : nullptr;
-    rcG = hd.recvConn >= 0 ? w.recv + (size_t)hd.recvConn * maxSplit + sub : nullptr;
-    static_assert(sizeof(DevSendConn) % 4 == 0 && sizeof(DevRecvConn) % 4 == 0, "connection copy");
-    constexpr int kSW = sizeof(DevSendConn) / 4, kRW = sizeof(DevRecvConn) / 4;
-    if (scG && tid < kSW) ((uint32_t*)&sh->sconn)[tid] = ((const uint32_t*)scG)[tid];
-    if (rcG && tid >= 64 && tid < 64 + kRW) ((uint32_t*)&sh->rconn)[tid - 64] = ((const uint32_t*)rcG)[tid - 64];
+    tr = (const DevTransfer*)&sh->img[1];
+    depBid = (const int16_t*)(tr + hd.nsteps);
+    depStep = depBid + hd.ndeps;
+    red = depStep + hd.ndeps;
+    scG = hd.hasSend ? w.send + cslot : nullptr;
+    rcG = hd.hasRecv ? w.recv + cslot : nullptr;
     sc = scG ? &sh->sconn : nullptr;
     rc = rcG ? &sh->rconn : nullptr;
-    if (tid == 0) {
-      sh->step[0] = scG ? scG->step : 0;
-      sh->step[1] = rcG ? rcG->step : 0;
-      sh->seen[0] = scG ? scG->headSeen : 0;
-      sh->seen[1] = rcG ? rcG->tailSeen : 0;
-      sh->aborted = 0;
-      sh->epoch = atomicLoadAgent(w.epochs + slot);
-    }
-    __syncthreads();
-    sendStep = uni(sh->step[0]);
-    recvStep = uni(sh->step[1]);
-    headSeen = uni(sh->seen[0]);
-    tailSeen = uni(sh->seen[1]);
-    trace = comm->trace ? comm->trace + (size_t)slot * comm->traceEvents : nullptr;
+    sendStep = scG ? uni(sh->sconn.step) : 0;
+    recvStep = rcG ? uni(sh->rconn.step) : 0;
+    headSeen = scG ? uni(sh->sconn.headSeen) : 0;
+    tailSeen = rcG ? uni(sh->rconn.tailSeen) : 0;
+    trace = w.trace ? w.trace + (size_t)slot * w.traceEvents : nullptr;
     nev = 1;
-    maxEv = comm->traceEvents;
+    maxEv = w.traceEvents;
     ev(kEvSetup, 0, 0);
 
     T* thisInput = (T*)w.sendbuff;
@@ -843,15 +842,15 @@ struct Interp {
       for (int i = 0; i < hd.nsteps; i++) {
         DevTransfer t;
         {
-          u32x4 raw = *(const u32x4*)&sh->tr[i];
+          u32x4 raw = *(const u32x4*)&tr[i];
           raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
           __builtin_memcpy(&t, &raw, sizeof(t));
         }
         if (t.numDeps > 0) {
           // the same positions of the thread blocks this transfer depends on (interpreter.h:123-140)
           if (tid < t.numDeps) {
-            const int db = sh->depBid[t.depPtr + tid];
-            const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)sh->depStep[t.depPtr + tid]);
+            const int db = depBid[t.depPtr + tid];
+            const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)depStep[t.depPtr + tid]);
             Spin spins;
             while (true) {
               uint64_t cur = atomicLoadAgent(flags + ((size_t)db * maxSplit + sub) * kFlagStride);
@@ -876,10 +875,10 @@ struct Interp {
         // sub-connection, and so far below the 2 GiB reach of a buffer descriptor.
         int macT = (t.type != tRe && !ringColl && nelem == sizePer &&
                     (int64_t)nelem * t.count <= w.maxOpElems) ? t.count : mac;
-        {
+        if ((int64_t)nelem * TS * macT > (int64_t)0x7fffff00) {
           // buffer descriptors address 2^31 - 1 bytes from a call's base (makeRsrc)
-          const int64_t reach = nelem > 0 ? (int64_t)0x7fffff00 / ((int64_t)nelem * TS) : 1;
-          if (macT > reach) macT = reach < 1 ? 1 : (int)reach;
+          const int64_t reach = (int64_t)0x7fffff00 / ((int64_t)nelem * TS);
+          macT = reach < 1 ? 1 : (int)reach;
         }
         for (int c = 0; c < t.count; c += macT) {
           int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
@@ -927,7 +926,7 @@ struct Interp {
             case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
             case tCopySend: op<0, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
             case tRe: {
-              reduce(srcP, sh->red + t.redPtr, grid + (int64_t)c * sizePer, sizePer, t.numReds, dstP + dstoff, s);
+              reduce(srcP, red + t.redPtr, grid + (int64_t)c * sizePer, sizePer, t.numReds, dstP + dstoff, s);
               if (c == 0) step += t.numReds - 1;
               __syncthreads();
               break;
@@ -960,11 +959,13 @@ struct Interp {
       atomicStoreAgent(w.epochs + slot, workIndex + 1);
     }
     {
-      // advance the epoch of every slot this launch does not run (DevComm::epochs): launch
-      // workgroup g covers the unlaunched slots j with j % launched == g
+      // advance the epoch of every slot this launch does not run (DevComm::epochs): the subs
+      // [split, maxSplit) of each launched tb (by that tb's sub 0), and the slots of the tbs
+      // beyond the schedule's, [nTb * maxSplit, kFlagSlots), dealt over the launch's workgroups
       const int launched = w.nBlocks, nTb = launched / split, g = bid * split + sub;
-      for (int j = g + tid * launched; j < kFlagSlots; j += kNT * launched)
-        if (j / maxSplit >= nTb || j % maxSplit >= split) atomicStoreAgent(w.epochs + j, workIndex + 1);
+      if (sub == 0 && tid < maxSplit - split) atomicStoreAgent(w.epochs + bid * maxSplit + split + tid, workIndex + 1);
+      for (int j = nTb * maxSplit + g + tid * launched; j < kFlagSlots; j += kNT * launched)
+        atomicStoreAgent(w.epochs + j, workIndex + 1);
     }
     ev(kEvEnd, 0, 0);
     if (trace != nullptr && tid == 0) {

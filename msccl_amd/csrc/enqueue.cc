@@ -132,13 +132,19 @@ RankWork makeRingWork(Planned& p) {
   w.recvbuff = p.op.recvbuff;
   w.scratch = comm->scratch;
   w.comm = comm->dComm;
-  w.send = comm->dSend;
-  w.recv = comm->dRecv;
+  w.send = da.dSend;
+  w.recv = da.dRecv;
+  w.connSplit = da.connSplit;
+  w.images = da.dImages;
+  w.tbStride = da.tbStride;
+  w.timeoutTicks = comm->timeoutTicks;
+  w.llFlagMask = comm->llFlagMask;
+  w.llCleanMask = comm->llCleanMask;
+  w.trace = comm->dTrace;
+  w.traceEvents = comm->traceEvents;
   w.flags = comm->dFlags;
   w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
   w.maxSplit = comm->maxSplit;
-  w.tbs = da.dTbs;
-  w.blob = da.dBlob;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;
   w.split = 1;
@@ -165,13 +171,19 @@ RankWork makeWork(Planned& p) {
   w.recvbuff = p.op.recvbuff;
   w.scratch = comm->scratch;
   w.comm = comm->dComm;
-  w.send = comm->dSend;
-  w.recv = comm->dRecv;
+  w.send = da.dSend;
+  w.recv = da.dRecv;
+  w.connSplit = da.connSplit;
+  w.images = da.dImages;
+  w.tbStride = da.tbStride;
+  w.timeoutTicks = comm->timeoutTicks;
+  w.llFlagMask = comm->llFlagMask;
+  w.llCleanMask = comm->llCleanMask;
+  w.trace = comm->dTrace;
+  w.traceEvents = comm->traceEvents;
   w.flags = comm->dFlags;
   w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
   w.maxSplit = comm->maxSplit;
-  w.tbs = da.dTbs;
-  w.blob = da.dBlob;
   w.sizePerChunk = p.plan.sizePerChunk;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;

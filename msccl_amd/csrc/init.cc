@@ -46,6 +46,11 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
   if (comm->nRanks > 1) NCCLCHECK(loadAlgos(comm));
   // 0 (default) = waits never time out, as in the reference; > 0 bounds every single wait
   comm->timeoutSec = (double)std::max<int64_t>(0, envInt("MSCCL_AMD_TIMEOUT_SEC", 0));
+  comm->timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
+  if (envInt("MSCCL_AMD_TEST_LL_CLEANUP", 0) != 0) {  // TEST_LL_CLEANUP (devcomm.h:56-63)
+    comm->llFlagMask = 0xffu;
+    comm->llCleanMask = 0x78u;
+  }
   comm->knobs = Knobs::fromEnv();
   comm->ringFallback = comm->knobs.ringFallback != 0;
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
@@ -159,16 +164,13 @@ ncclResult_t commFinish(ncclComm* comm) {
   NCCLCHECK(algoUpload(comm));
   DevComm dc;
   memset(&dc, 0, sizeof(dc));
-  dc.send = comm->dSend;
-  dc.recv = comm->dRecv;
   dc.flags = comm->dFlags;
   dc.abortFlag = comm->devAbort;
   dc.errWord = comm->devErr;
-  dc.timeoutTicks = (uint64_t)(comm->timeoutSec * 1e8);  // s_memrealtime runs at 100 MHz
+  dc.timeoutTicks = comm->timeoutTicks;
   dc.maxSplit = comm->maxSplit;
-  const bool llTest = envInt("MSCCL_AMD_TEST_LL_CLEANUP", 0) != 0;  // TEST_LL_CLEANUP (devcomm.h:56-63)
-  dc.llFlagMask = llTest ? 0xffu : 0xffffffffu;
-  dc.llCleanMask = llTest ? 0x78u : 0x7ffffff8u;
+  dc.llFlagMask = comm->llFlagMask;
+  dc.llCleanMask = comm->llCleanMask;
   if (envInt("MSCCL_AMD_TRACE", 0) > 0) {
     comm->traceEvents = (int)std::max<int64_t>(8, std::min<int64_t>(65535, envInt("MSCCL_AMD_TRACE_EVENTS", 256)));
     size_t bytes = (size_t)kMaxTb * comm->maxSplit * comm->traceEvents * sizeof(TraceEvent);
@@ -265,17 +267,16 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
   hipSetDevice(comm->cudaDev);
   hipDeviceSynchronize();
   for (auto& d : comm->devAlgos) {
-    if (d.dTbs) hipFree(d.dTbs);
-    if (d.dBlob) hipFree(d.dBlob);
+    if (d.dImages) hipFree(d.dImages);
+    if (d.dSend) hipFree(d.dSend);
+    if (d.dRecv) hipFree(d.dRecv);
   }
-  for (auto& d : comm->ringAlgos) {
-    if (d.dTbs) hipFree(d.dTbs);
-    if (d.dBlob) hipFree(d.dBlob);
-  }
+  for (auto& d : comm->ringAlgos)
+    if (d.dImages) hipFree(d.dImages);  // their connection records are comm->ringSend / ringRecv
+  if (comm->ringSend) hipFree(comm->ringSend);
+  if (comm->ringRecv) hipFree(comm->ringRecv);
   for (size_t r = 0; r < comm->peerArena.size(); r++)
     if (comm->peerArenaIpc[r] && comm->peerArena[r]) hipIpcCloseMemHandle(comm->peerArena[r]);
-  if (comm->dSend) hipFree(comm->dSend);
-  if (comm->dRecv) hipFree(comm->dRecv);
   if (comm->dComm) hipFree(comm->dComm);
   if (comm->dFlags) hipFree(comm->dFlags);
   if (comm->dTrace) hipFree(comm->dTrace);

@@ -2,12 +2,17 @@
 //
 // Replaces the reference's P2P transport (transport/p2p.cc:143-344) and the MSCCL connect block
 // of initTransportsRank (init.cc:781-874):
-//   * one connection per (channel, peer) and direction, as named by the XML thread blocks;
-//   * the receiver owns the FIFOs (LL: 8 steps x 4096 16-B lines; Simple: 8 x 512 KiB by
-//     default, NCCL_LL_BUFFSIZE / NCCL_BUFFSIZE override) and a tail word; the sender owns a
-//     head word the receiver writes.  All of it lives in one uncached (fine-grained) HBM arena
-//     per rank, exported once per rank (hipIpc) or shared by pointer inside a process;
-//   * a rank's layout is published as a table [channel][peer] -> offsets and exchanged.
+//   * one connection per (channel, peer) and direction, as named by the XML thread blocks.  The
+//     reference shares a (channel, peer) connection between all loaded algorithms; here every
+//     algorithm (and the ring fallback) owns its connections, so a connection belongs to exactly
+//     one (algorithm, thread block, sub-workgroup) and its persistent step counters sit at an
+//     address the kernel computes from its block index alone (no dependent load in the kernel
+//     prologue).  The FIFO memory this costs is small next to 288 GB of HBM;
+//   * the receiver owns the FIFOs (LL: 8 steps x 4096 16-B lines; Simple: 8 x 512 KiB by default,
+//     NCCL_LL_BUFFSIZE / NCCL_BUFFSIZE override) and a tail word; the sender owns a head word the
+//     receiver writes.  All of it lives in one uncached (fine-grained) HBM arena per rank,
+//     exported once per rank (hipIpc) or shared by pointer inside a process;
+//   * a rank's layout is published as a table [group][channel][peer] -> offsets and exchanged.
 #include <hip/hip_runtime.h>
 #include <string.h>
 
@@ -23,7 +28,26 @@ namespace {
 constexpr size_t kWordStride = 128;   // head/tail words on their own 128-B lines
 constexpr size_t kFifoAlign = 4096;
 size_t alignUp(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Protocols whose FIFO memory a group needs (LL and LL128 share the LL FIFO).
+uint8_t groupProtoMask(const ncclComm* comm, int group) {
+  if (group == kRingGroup) return (uint8_t)((1u << kProtoLL) | (1u << kProtoSimple));
+  uint8_t m = (uint8_t)(1u << comm->algos[group].proto);
+  for (auto& r : comm->regs)
+    if (r.algoIndex == group) m |= (uint8_t)(1u << r.proto);
+  if (m & (1u << kProtoLL128)) m |= (uint8_t)(1u << kProtoLL);  // LL128 may run as LL (remote peers)
+  return m;
+}
+
+int groupSubs(const ncclComm* comm, int group) {
+  if (group == kRingGroup) return 1;  // the ring runs unsplit
+  return comm->algoSplit.empty() ? 1 : comm->algoSplit[group];
+}
 }  // namespace
+
+size_t tableIndex(int group, int chan, int peer, int nRanks) {
+  return ((size_t)group * kMaxChannels + chan) * nRanks + peer;
+}
 
 ncclResult_t transportPlan(ncclComm* comm) {
   const int n = comm->nRanks;
@@ -41,76 +65,71 @@ ncclResult_t transportPlan(ncclComm* comm) {
     WARN("MSCCL: FIFO buffer sizes too small (LL %d, Simple %d)", comm->buffSizes[0], comm->buffSizes[2]);
     return ncclInvalidArgument;
   }
-  std::map<ConnKey, uint8_t> sends, recvs;
-  for (auto& a : comm->algos) {
-    std::map<ConnKey, int> seenS, seenR;
+  if (comm->algos.size() > (size_t)kMaxAlgos) {
+    WARN("MSCCL: %zu algorithms loaded, at most %d", comm->algos.size(), kMaxAlgos);
+    return ncclInternalError;
+  }
+  comm->sendKeys.clear();
+  comm->recvKeys.clear();
+  for (size_t g = 0; g < comm->algos.size(); g++) {
+    const Algorithm& a = comm->algos[g];
+    std::map<std::pair<int, int>, int> seenS, seenR;
     for (int b = 0; b < a.nBlocks; b++) {
       const ThreadBlock& tb = a.tbs[b];
-      uint8_t bit = (uint8_t)(1u << a.proto);
       if (tb.sendpeer >= 0) {
-        ConnKey k{tb.channel, tb.sendpeer};
+        auto k = std::make_pair((int)tb.channel, (int)tb.sendpeer);
         if (seenS.count(k)) {
           WARN("MSCCL: algorithm %s: thread blocks %d and %d both send to peer %d on channel %d",
                a.name.c_str(), seenS[k], b, tb.sendpeer, tb.channel);
           return ncclInvalidUsage;
         }
         seenS[k] = b;
-        sends[k] |= bit;
+        comm->sendKeys.push_back(ConnKey{(int)g, tb.channel, tb.sendpeer});
       }
       if (tb.recvpeer >= 0) {
-        ConnKey k{tb.channel, tb.recvpeer};
+        auto k = std::make_pair((int)tb.channel, (int)tb.recvpeer);
         if (seenR.count(k)) {
           WARN("MSCCL: algorithm %s: thread blocks %d and %d both receive from peer %d on channel %d",
                a.name.c_str(), seenR[k], b, tb.recvpeer, tb.channel);
           return ncclInvalidUsage;
         }
         seenR[k] = b;
-        recvs[k] |= bit;
+        comm->recvKeys.push_back(ConnKey{(int)g, tb.channel, tb.recvpeer});
       }
     }
   }
-  // ring fallback connections: one ring per channel kRingChanBase + c (send to rank+1, receive
-  // from rank-1), LL and Simple FIFOs, one sub-connection each (the ring runs unsplit)
+  // ring fallback: ring channel c sends to rank+1 and receives from rank-1 (one sub-connection)
   if (comm->ringFallback && n > 1) {
-    const uint8_t bits = (uint8_t)((1u << kProtoLL) | (1u << kProtoSimple));
     for (int c = 0; c < kRingChannels; c++) {
-      sends[ConnKey{kRingChanBase + c, (comm->rank + 1) % n}] |= bits;
-      recvs[ConnKey{kRingChanBase + c, (comm->rank + n - 1) % n}] |= bits;
+      comm->sendKeys.push_back(ConnKey{kRingGroup, c, (comm->rank + 1) % n});
+      comm->recvKeys.push_back(ConnKey{kRingGroup, c, (comm->rank + n - 1) % n});
     }
   }
-  comm->sendKeys.clear();
-  comm->recvKeys.clear();
-  comm->sendProtoMask.clear();
-  comm->recvProtoMask.clear();
-  for (auto& kv : sends) { comm->sendKeys.push_back(kv.first); comm->sendProtoMask.push_back(kv.second); }
-  for (auto& kv : recvs) { comm->recvKeys.push_back(kv.first); comm->recvProtoMask.push_back(kv.second); }
-
-  const int S = comm->maxSplit;
   const int64_t llBytes = (int64_t)alignUp((size_t)kLLFifoSlots * comm->llSlotLines * 16, kFifoAlign);
   const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
-  comm->table.assign((size_t)kTableChannels * n, PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
-  // ring keys have a single sub-connection: stride 0 makes every sub alias sub 0
-  auto subsOf = [&](const ConnKey& k) { return k.chan >= kRingChanBase ? 1 : S; };
-  for (int c = kRingChanBase; c < kTableChannels; c++)
-    for (int p = 0; p < n; p++) {
-      PeerOffsets& po = comm->table[(size_t)c * n + p];
-      po.llStride = po.simpleStride = po.wordStride = 0;
-    }
+  comm->table.assign((size_t)(kMaxAlgos + 1) * kMaxChannels * n,
+                     PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
   size_t off = 0;
-  for (auto& k : comm->sendKeys) { comm->table[(size_t)k.chan * n + k.peer].sendHead = (int64_t)off; off += kWordStride * subsOf(k); }
-  for (auto& k : comm->recvKeys) { comm->table[(size_t)k.chan * n + k.peer].recvTail = (int64_t)off; off += kWordStride * subsOf(k); }
+  for (auto& k : comm->sendKeys) {
+    comm->table[tableIndex(k.group, k.chan, k.peer, n)].sendHead = (int64_t)off;
+    off += kWordStride * groupSubs(comm, k.group);
+  }
+  for (auto& k : comm->recvKeys) {
+    comm->table[tableIndex(k.group, k.chan, k.peer, n)].recvTail = (int64_t)off;
+    off += kWordStride * groupSubs(comm, k.group);
+  }
   off = alignUp(off, kFifoAlign);
-  for (size_t i = 0; i < comm->recvKeys.size(); i++) {
-    auto& k = comm->recvKeys[i];
-    PeerOffsets& po = comm->table[(size_t)k.chan * n + k.peer];
-    // LL and LL128 share the LL FIFO memory (two line formats)
-    if (comm->recvProtoMask[i] & ((1u << kProtoLL) | (1u << kProtoLL128))) {
+  for (auto& k : comm->recvKeys) {
+    PeerOffsets& po = comm->table[tableIndex(k.group, k.chan, k.peer, n)];
+    const uint8_t m = groupProtoMask(comm, k.group);
+    const int subs = groupSubs(comm, k.group);
+    if (m & ((1u << kProtoLL) | (1u << kProtoLL128))) {  // LL and LL128 share the LL FIFO memory
       po.recvLL = (int64_t)off;
-      off += (size_t)llBytes * subsOf(k);
+      off += (size_t)llBytes * subs;
     }
-    if (comm->recvProtoMask[i] & (1u << kProtoSimple)) {
+    if (m & (1u << kProtoSimple)) {
       po.recvSimple = (int64_t)off;
-      off += (size_t)simpleBytes * subsOf(k);
+      off += (size_t)simpleBytes * subs;
     }
   }
   comm->arenaSize = off ? off : kFifoAlign;
@@ -127,65 +146,132 @@ ncclResult_t transportPlan(ncclComm* comm) {
   return ncclSuccess;
 }
 
+// Build and upload the slot-indexed connection records of one group: entry tb * subs + sub.
+static ncclResult_t buildConns(ncclComm* comm, int group, int nTb, const std::vector<int>& sendPeer,
+                               const std::vector<int>& recvPeer, const std::vector<int>& chan,
+                               const std::vector<std::vector<PeerOffsets>>& tables, const std::vector<char*>& peerBases,
+                               const std::vector<int>& peerRemote, DevSendConn** dS, DevRecvConn** dR) {
+  const int n = comm->nRanks, me = comm->rank, S = groupSubs(comm, group);
+  const uint8_t m = groupProtoMask(comm, group);
+  const bool needLL = m & ((1u << kProtoLL) | (1u << kProtoLL128)), needS = m & (1u << kProtoSimple);
+  std::vector<DevSendConn> hs((size_t)std::max(nTb, 1) * S);
+  std::vector<DevRecvConn> hr((size_t)std::max(nTb, 1) * S);
+  memset(hs.data(), 0, hs.size() * sizeof(DevSendConn));
+  memset(hr.data(), 0, hr.size() * sizeof(DevRecvConn));
+  for (int b = 0; b < nTb; b++) {
+    if (sendPeer[b] >= 0) {
+      const int p = sendPeer[b];
+      const PeerOffsets& theirs = tables[p][tableIndex(group, chan[b], me, n)];
+      const PeerOffsets& mine = comm->table[tableIndex(group, chan[b], p, n)];
+      if (theirs.recvTail < 0 || (needLL && theirs.recvLL < 0) || (needS && theirs.recvSimple < 0)) {
+        WARN("MSCCL: rank %d sends to rank %d on channel %d but rank %d has no matching receive", me, p, chan[b], p);
+        return ncclInvalidUsage;
+      }
+      char* pb = peerBases[p];
+      for (int s = 0; s < S; s++) {
+        DevSendConn& c = hs[(size_t)b * S + s];
+        c.ll = theirs.recvLL >= 0 ? (LLLine*)(pb + theirs.recvLL + s * theirs.llStride) : nullptr;
+        c.simple = theirs.recvSimple >= 0 ? pb + theirs.recvSimple + s * theirs.simpleStride : nullptr;
+        c.remoteTail = (uint64_t*)(pb + theirs.recvTail + s * theirs.wordStride);
+        c.head = (uint64_t*)(comm->arena + mine.sendHead + s * mine.wordStride);
+        c.llSlotLines = comm->llSlotLines;
+        c.simpleSlotBytes = comm->simpleSlotBytes;
+        c.remote = peerRemote[p];
+      }
+    }
+    if (recvPeer[b] >= 0) {
+      const int p = recvPeer[b];
+      const PeerOffsets& theirs = tables[p][tableIndex(group, chan[b], me, n)];
+      const PeerOffsets& mine = comm->table[tableIndex(group, chan[b], p, n)];
+      if (theirs.sendHead < 0) {
+        WARN("MSCCL: rank %d receives from rank %d on channel %d but rank %d has no matching send", me, p, chan[b],
+             p);
+        return ncclInvalidUsage;
+      }
+      for (int s = 0; s < S; s++) {
+        DevRecvConn& c = hr[(size_t)b * S + s];
+        c.ll = mine.recvLL >= 0 ? (LLLine*)(comm->arena + mine.recvLL + s * mine.llStride) : nullptr;
+        c.simple = mine.recvSimple >= 0 ? comm->arena + mine.recvSimple + s * mine.simpleStride : nullptr;
+        c.tail = (uint64_t*)(comm->arena + mine.recvTail + s * mine.wordStride);
+        c.remoteHead = (uint64_t*)(peerBases[p] + theirs.sendHead + s * theirs.wordStride);
+        c.llSlotLines = comm->llSlotLines;
+        c.simpleSlotBytes = comm->simpleSlotBytes;
+      }
+    }
+  }
+  if (hipMalloc(dS, hs.size() * sizeof(DevSendConn)) != hipSuccess) return ncclUnhandledCudaError;
+  if (hipMalloc(dR, hr.size() * sizeof(DevRecvConn)) != hipSuccess) return ncclUnhandledCudaError;
+  if (hipMemcpy(*dS, hs.data(), hs.size() * sizeof(DevSendConn), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(*dR, hr.data(), hr.size() * sizeof(DevRecvConn), hipMemcpyHostToDevice) != hipSuccess)
+    return ncclUnhandledCudaError;
+  return ncclSuccess;
+}
+
 ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<PeerOffsets>>& tables,
                               const std::vector<char*>& peerBases, const std::vector<int>& peerRemote) {
-  const int n = comm->nRanks, me = comm->rank, S = comm->maxSplit;
-  std::vector<DevSendConn> hs(comm->sendKeys.size() * S);
-  std::vector<DevRecvConn> hr(comm->recvKeys.size() * S);
-  for (size_t i = 0; i < comm->sendKeys.size(); i++) {
-    const ConnKey& k = comm->sendKeys[i];
-    const PeerOffsets& theirs = tables[k.peer][(size_t)k.chan * n + me];
-    const PeerOffsets& mine = comm->table[(size_t)k.chan * n + k.peer];
-    uint8_t need = comm->sendProtoMask[i];
-    bool needLL = need & ((1u << kProtoLL) | (1u << kProtoLL128)), needS = need & (1u << kProtoSimple);
-    if (theirs.recvTail < 0 || (needLL && theirs.recvLL < 0) || (needS && theirs.recvSimple < 0)) {
-      WARN("MSCCL: rank %d sends to rank %d on channel %d but rank %d has no matching receive", me, k.peer,
-           k.chan, k.peer);
-      return ncclInvalidUsage;
+  const int n = comm->nRanks;
+  comm->devAlgos.assign(comm->algos.size(), DevAlgoHost());
+  for (size_t g = 0; g < comm->algos.size(); g++) {
+    const Algorithm& a = comm->algos[g];
+    std::vector<int> sp(a.nBlocks), rp(a.nBlocks), ch(a.nBlocks);
+    for (int b = 0; b < a.nBlocks; b++) {
+      sp[b] = a.tbs[b].sendpeer;
+      rp[b] = a.tbs[b].recvpeer;
+      ch[b] = a.tbs[b].channel;
     }
-    char* pb = peerBases[k.peer];
-    for (int s = 0; s < S; s++) {
-      DevSendConn& c = hs[i * S + s];
-      memset(&c, 0, sizeof(c));
-      c.ll = theirs.recvLL >= 0 ? (LLLine*)(pb + theirs.recvLL + s * theirs.llStride) : nullptr;
-      c.simple = theirs.recvSimple >= 0 ? pb + theirs.recvSimple + s * theirs.simpleStride : nullptr;
-      c.remoteTail = (uint64_t*)(pb + theirs.recvTail + s * theirs.wordStride);
-      c.head = (uint64_t*)(comm->arena + mine.sendHead + s * mine.wordStride);
-      c.step = 0;
-      c.llSlotLines = comm->llSlotLines;
-      c.simpleSlotBytes = comm->simpleSlotBytes;
-      c.remote = peerRemote[k.peer];
-    }
+    DevAlgoHost& d = comm->devAlgos[g];
+    d.connSplit = groupSubs(comm, (int)g);
+    NCCLCHECK(buildConns(comm, (int)g, a.nBlocks, sp, rp, ch, tables, peerBases, peerRemote, &d.dSend, &d.dRecv));
   }
-  for (size_t i = 0; i < comm->recvKeys.size(); i++) {
-    const ConnKey& k = comm->recvKeys[i];
-    const PeerOffsets& theirs = tables[k.peer][(size_t)k.chan * n + me];
-    const PeerOffsets& mine = comm->table[(size_t)k.chan * n + k.peer];
-    if (theirs.sendHead < 0) {
-      WARN("MSCCL: rank %d receives from rank %d on channel %d but rank %d has no matching send", me, k.peer,
-           k.chan, k.peer);
-      return ncclInvalidUsage;
-    }
-    for (int s = 0; s < S; s++) {
-      DevRecvConn& c = hr[i * S + s];
-      memset(&c, 0, sizeof(c));
-      c.ll = mine.recvLL >= 0 ? (LLLine*)(comm->arena + mine.recvLL + s * mine.llStride) : nullptr;
-      c.simple = mine.recvSimple >= 0 ? comm->arena + mine.recvSimple + s * mine.simpleStride : nullptr;
-      c.tail = (uint64_t*)(comm->arena + mine.recvTail + s * mine.wordStride);
-      c.remoteHead = (uint64_t*)(peerBases[k.peer] + theirs.sendHead + s * theirs.wordStride);
-      c.step = 0;
-      c.llSlotLines = comm->llSlotLines;
-      c.simpleSlotBytes = comm->simpleSlotBytes;
-    }
+  if (comm->ringFallback && n > 1) {
+    std::vector<int> sp(kRingChannels, (comm->rank + 1) % n), rp(kRingChannels, (comm->rank + n - 1) % n),
+        ch(kRingChannels);
+    for (int c = 0; c < kRingChannels; c++) ch[c] = c;
+    NCCLCHECK(buildConns(comm, kRingGroup, kRingChannels, sp, rp, ch, tables, peerBases, peerRemote, &comm->ringSend,
+                         &comm->ringRecv));
   }
-  if (!hs.empty()) {
-    if (hipMalloc(&comm->dSend, hs.size() * sizeof(DevSendConn)) != hipSuccess) return ncclUnhandledCudaError;
-    hipMemcpy(comm->dSend, hs.data(), hs.size() * sizeof(DevSendConn), hipMemcpyHostToDevice);
+  return ncclSuccess;
+}
+
+// Thread-block image: [DevTbHeader][nsteps DevTransfer][ndeps int16 bid][ndeps int16 step]
+// [nreds int16 source offsets], padded to 16 B.  Every image of a group has the same stride, so
+// a workgroup finds its own from its block index (devcomm.h).
+static void putImage(std::vector<char>& out, size_t at, const DevTbHeader& h, const std::vector<Transfer>& ts,
+                     const std::vector<int16_t>& depBid, const std::vector<int16_t>& depStep,
+                     const std::vector<int16_t>& reds) {
+  char* p = out.data() + at;
+  memcpy(p, &h, sizeof(h));
+  p += sizeof(h);
+  for (const Transfer& t : ts) {
+    DevTransfer x;
+    memset(&x, 0, sizeof(x));
+    x.srcoff = t.srcoff;
+    x.dstoff = t.dstoff;
+    x.srcbuf = t.srcbuf;
+    x.dstbuf = t.dstbuf;
+    x.type = t.type;
+    x.count = t.count;
+    x.depPtr = t.depPtr;
+    x.numDeps = t.numDeps;
+    x.redPtr = t.redPtr;
+    x.numReds = (uint8_t)t.numReds;
+    x.hasDep = (uint8_t)t.hasDep;
+    memcpy(p, &x, sizeof(x));
+    p += sizeof(x);
   }
-  if (!hr.empty()) {
-    if (hipMalloc(&comm->dRecv, hr.size() * sizeof(DevRecvConn)) != hipSuccess) return ncclUnhandledCudaError;
-    hipMemcpy(comm->dRecv, hr.data(), hr.size() * sizeof(DevRecvConn), hipMemcpyHostToDevice);
+  for (const std::vector<int16_t>* v : {&depBid, &depStep, &reds}) {
+    if (!v->empty()) memcpy(p, v->data(), v->size() * sizeof(int16_t));
+    p += v->size() * sizeof(int16_t);
   }
+}
+
+static size_t imageBytes(size_t nsteps, size_t ndeps, size_t nreds) {
+  return alignUp(sizeof(DevTbHeader) + nsteps * sizeof(DevTransfer) + (2 * ndeps + nreds) * sizeof(int16_t), 16);
+}
+
+static ncclResult_t uploadImages(const std::vector<char>& img, DevAlgoHost* d) {
+  if (hipMalloc(&d->dImages, img.size()) != hipSuccess) return ncclUnhandledCudaError;
+  if (hipMemcpy(d->dImages, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return ncclUnhandledCudaError;
   return ncclSuccess;
 }
 
@@ -230,52 +316,28 @@ static std::vector<Transfer> ringProgram(int kind, int r, int n) {
 ncclResult_t ringUpload(ncclComm* comm) {
   const int n = comm->nRanks;
   if (!comm->ringFallback || n < 2) return ncclSuccess;
-  int sendIdx[kRingChannels], recvIdx[kRingChannels];
-  for (int c = 0; c < kRingChannels; c++) {
-    sendIdx[c] = recvIdx[c] = -1;
-    for (size_t i = 0; i < comm->sendKeys.size(); i++)
-      if (comm->sendKeys[i] == ConnKey{kRingChanBase + c, (comm->rank + 1) % n}) sendIdx[c] = (int)i;
-    for (size_t i = 0; i < comm->recvKeys.size(); i++)
-      if (comm->recvKeys[i] == ConnKey{kRingChanBase + c, (comm->rank + n - 1) % n}) recvIdx[c] = (int)i;
-    if (sendIdx[c] < 0 || recvIdx[c] < 0) return ncclInternalError;
-  }
+  const std::vector<int16_t> none;
   for (int kind = 0; kind < 4; kind++) {
     const std::vector<Transfer> prog = ringProgram(kind, comm->rank, n);
-    std::vector<DevTbHeader> hdr(kRingChannels);
-    std::vector<char> blob;
-    for (const Transfer& t : prog) {
-      DevTransfer x;
-      memset(&x, 0, sizeof(x));
-      x.srcoff = t.srcoff;
-      x.dstoff = t.dstoff;
-      x.srcbuf = t.srcbuf;
-      x.dstbuf = t.dstbuf;
-      x.type = t.type;
-      x.count = t.count;
-      const char* p = (const char*)&x;
-      blob.insert(blob.end(), p, p + sizeof(x));
-    }
-    blob.resize(alignUp(blob.size() + 16, 16));
-    for (int c = 0; c < kRingChannels; c++) {  // every channel runs the same program
-      DevTbHeader& h = hdr[c];
-      memset(&h, 0, sizeof(h));
-      h.sendConn = (int16_t)sendIdx[c];
-      h.recvConn = (int16_t)recvIdx[c];
-      h.nsteps = (uint16_t)prog.size();
-      h.blobOffset = 0;
-    }
     DevAlgoHost& d = comm->ringAlgos[kind];
     d.nBlocks = kRingChannels;
-    if (hipMalloc(&d.dTbs, hdr.size() * sizeof(DevTbHeader)) != hipSuccess) return ncclUnhandledCudaError;
-    if (hipMalloc(&d.dBlob, blob.size()) != hipSuccess) return ncclUnhandledCudaError;
-    hipMemcpy(d.dTbs, hdr.data(), hdr.size() * sizeof(DevTbHeader), hipMemcpyHostToDevice);
-    hipMemcpy(d.dBlob, blob.data(), blob.size(), hipMemcpyHostToDevice);
+    d.tbStride = (int)imageBytes(prog.size(), 0, 0);
+    d.connSplit = 1;
+    d.dSend = comm->ringSend;  // owned by the communicator, shared by the four ring programs
+    d.dRecv = comm->ringRecv;
+    std::vector<char> img((size_t)d.tbStride * kRingChannels, 0);
+    for (int c = 0; c < kRingChannels; c++) {  // every channel runs the same program
+      DevTbHeader h;
+      memset(&h, 0, sizeof(h));
+      h.hasSend = h.hasRecv = 1;
+      h.nsteps = (uint16_t)prog.size();
+      putImage(img, (size_t)c * d.tbStride, h, prog, none, none, none);
+    }
+    NCCLCHECK(uploadImages(img, &d));
   }
   return ncclSuccess;
 }
 
-// Pack every algorithm's per-tb programs and upload them (replaces the 29 MB
-// mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 // Longest run of chunks a thread block sends before it next receives (merge bound, devcomm.h).
 int algoSendRunOf(const Algorithm& a) {
   int best = 0;
@@ -291,59 +353,33 @@ int algoSendRunOf(const Algorithm& a) {
   return best;
 }
 
+// Pack every algorithm's per-tb programs into fixed-stride images and upload them (replaces
+// the 29 MB mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 ncclResult_t algoUpload(ncclComm* comm) {
-  comm->devAlgos.clear();
-  for (auto& a : comm->algos) {
-    DevAlgoHost d;
+  for (size_t g = 0; g < comm->algos.size(); g++) {
+    const Algorithm& a = comm->algos[g];
+    if (g >= comm->devAlgos.size()) comm->devAlgos.resize(g + 1);
+    DevAlgoHost& d = comm->devAlgos[g];
     d.nBlocks = a.nBlocks;
-    std::vector<DevTbHeader> hdr(a.nBlocks > 0 ? a.nBlocks : 1);
-    std::vector<char> blob;
+    size_t stride = 16;
     for (int b = 0; b < a.nBlocks; b++) {
       const ThreadBlock& tb = a.tbs[b];
-      DevTbHeader& h = hdr[b];
+      stride = std::max(stride, imageBytes(tb.transfers.size(), tb.depBid.size(), tb.redSrcOff.size()));
+    }
+    d.tbStride = (int)stride;
+    std::vector<char> img(stride * std::max(a.nBlocks, 1), 0);
+    for (int b = 0; b < a.nBlocks; b++) {
+      const ThreadBlock& tb = a.tbs[b];
+      DevTbHeader h;
       memset(&h, 0, sizeof(h));
-      h.sendConn = h.recvConn = -1;
-      for (size_t i = 0; i < comm->sendKeys.size(); i++)
-        if (tb.sendpeer >= 0 && comm->sendKeys[i] == ConnKey{tb.channel, tb.sendpeer}) h.sendConn = (int16_t)i;
-      for (size_t i = 0; i < comm->recvKeys.size(); i++)
-        if (tb.recvpeer >= 0 && comm->recvKeys[i] == ConnKey{tb.channel, tb.recvpeer}) h.recvConn = (int16_t)i;
+      h.hasSend = tb.sendpeer >= 0;
+      h.hasRecv = tb.recvpeer >= 0;
       h.nsteps = tb.nsteps;
       h.ndeps = (uint16_t)tb.depBid.size();
       h.nreds = (uint16_t)tb.redSrcOff.size();
-      size_t start = alignUp(blob.size(), 16);
-      blob.resize(start);
-      h.blobOffset = (uint32_t)start;
-      for (const Transfer& t : tb.transfers) {
-        DevTransfer x;
-        memset(&x, 0, sizeof(x));
-        x.srcoff = t.srcoff;
-        x.dstoff = t.dstoff;
-        x.srcbuf = t.srcbuf;
-        x.dstbuf = t.dstbuf;
-        x.type = t.type;
-        x.count = t.count;
-        x.depPtr = t.depPtr;
-        x.numDeps = t.numDeps;
-        x.redPtr = t.redPtr;
-        x.numReds = (uint8_t)t.numReds;
-        x.hasDep = (uint8_t)t.hasDep;
-        const char* p = (const char*)&x;
-        blob.insert(blob.end(), p, p + sizeof(x));
-      }
-      auto put16 = [&](const std::vector<int16_t>& v) {
-        const char* p = (const char*)v.data();
-        blob.insert(blob.end(), p, p + v.size() * sizeof(int16_t));
-      };
-      put16(tb.depBid);
-      put16(tb.depStep);
-      put16(tb.redSrcOff);
+      putImage(img, (size_t)b * stride, h, tb.transfers, tb.depBid, tb.depStep, tb.redSrcOff);
     }
-    blob.resize(alignUp(blob.size() + 16, 16));
-    if (hipMalloc(&d.dTbs, hdr.size() * sizeof(DevTbHeader)) != hipSuccess) return ncclUnhandledCudaError;
-    if (hipMalloc(&d.dBlob, blob.size()) != hipSuccess) return ncclUnhandledCudaError;
-    hipMemcpy(d.dTbs, hdr.data(), hdr.size() * sizeof(DevTbHeader), hipMemcpyHostToDevice);
-    hipMemcpy(d.dBlob, blob.data(), blob.size(), hipMemcpyHostToDevice);
-    comm->devAlgos.push_back(d);
+    NCCLCHECK(uploadImages(img, &d));
   }
   return ringUpload(comm);
 }

@@ -207,6 +207,31 @@ def allreduce_oneshot(n: int, instances: int = 1, proto: str = "LL",
     return _emit(name, proto, I, I, n, "allreduce", True, gpus, min_bytes, max_bytes, nthreads)
 
 
+def allreduce_pair_oneshot(instances: int = 1, proto: str = "LL", inplace: bool = True,
+                           min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
+                           nthreads: Optional[int] = None, name: str = "allreduce_pair_oneshot") -> str:
+    """Two-rank all-pairs AllReduce in one hop: thread block k of each rank sends its chunk k to
+    the peer and receives the peer's chunk k, reducing it with its own into the output (`s`,
+    `rrc`).  No scratch, no cross-tb dependency: one FIFO hand-off on the critical path.  The
+    reduce is fn(peer, local) (LL) on one rank and its mirror on the other, so both ranks hold
+    the same bits for a commutative op."""
+    I = instances
+    gpus = {}
+    ob = "i" if inplace else "o"
+    for r in range(2):
+        p = 1 - r
+        tbs = []
+        for k in range(I):
+            tb = _Tb(k, p, p, k)
+            tb.add("s", "i", k, ob, k, 1)
+            tb.add("rrc", "i", k, ob, k, 1)
+            tbs.append(tb)
+        gpus[r] = (I, 0 if inplace else I, 0, tbs)
+    if max_bytes is None:
+        max_bytes = 1 << 62
+    return _emit(name, proto, I, I, 2, "allreduce", inplace, gpus, min_bytes, max_bytes, nthreads)
+
+
 def _slot_of(r: int, p: int) -> int:
     """scratch slot of sender r on receiver p: peers of p in ascending order, p skipped."""
     return r if r < p else r - 1

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
 from oracle import loader as L  # noqa: E402
-from tests.test_gpu_alltoall import RCCL, run_xml  # noqa: E402
+from tests.test_gpu_widening_alltoall import RCCL, run_xml  # noqa: E402
 
 NAMES = ["alltoall-8n-0-9kb.xml", "alltoall-8n-9kb-190kb.xml", "alltoall-8n-190kb-512kb.xml",
          "alltoall-8n-512kb-7mb.xml", "alltoall-8n-7mb-43mb.xml"]

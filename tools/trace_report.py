@@ -28,10 +28,15 @@ def main():
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--instances", type=int, default=1)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--schedule", default="allpairs", choices=["allpairs", "pair", "ring", "oneshot"])
     a = ap.parse_args()
     import torch
     path = "/tmp/trace_ap_%d.xml" % os.getpid()
-    open(path, "w").write(xmlgen.allreduce_allpairs(a.ranks, a.instances, a.proto))
+    gen = {"allpairs": lambda: xmlgen.allreduce_allpairs(a.ranks, a.instances, a.proto),
+           "pair": lambda: xmlgen.allreduce_pair_oneshot(a.instances, a.proto),
+           "ring": lambda: xmlgen.allreduce_ring(a.ranks, a.instances, a.proto),
+           "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2)}
+    open(path, "w").write(gen[a.schedule]())
     os.environ["MSCCL_XML_FILES"] = path
     comms = M.Comm.init_all([0] * a.ranks)
     cnt = a.bytes // 4
