@@ -102,8 +102,10 @@ typedef enum {
   ncclScalarHostImmediate = 1
 } ncclScalarResidence_t;
 
-/* nccl.h.in:163,173 — PreMulSum user ops are never MSCCL-eligible in the
- * reference (tuning.cc:345); this build returns ncclInvalidUsage for them. */
+/* nccl.h.in:153-174.  Creates a PreMulSum user op: every input is multiplied by *scalar before
+ * the sum (the scalar is read at call time from host memory, ncclScalarHostImmediate, or at
+ * kernel time from device memory, ncclScalarDevice).  Like ncclAvg, such ops are never
+ * MSCCL-eligible (tuning.cc:345): they run on the ring fallback. */
 ncclResult_t  ncclRedOpCreatePreMulSum(ncclRedOp_t *op, void *scalar, ncclDataType_t datatype, ncclScalarResidence_t residence, ncclComm_t comm);
 ncclResult_t  ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm);
 

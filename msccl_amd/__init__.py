@@ -31,6 +31,7 @@ TYPE_SIZE = {INT8: 1, UINT8: 1, INT32: 4, UINT32: 4, INT64: 8, UINT64: 8, FLOAT1
              FLOAT64: 8, BFLOAT16: 2}
 # ncclRedOp_t (nccl.h.in:106-121)
 SUM, PROD, MAX, MIN, AVG = range(5)
+SCALAR_DEVICE, SCALAR_HOST = 0, 1  # ncclScalarResidence_t
 # ncclFunc_t (devcomm.h:16)
 COLL_ALLGATHER, COLL_REDUCE_SCATTER, COLL_ALLREDUCE, COLL_ALLTOALL, COLL_CUSTOM = 2, 3, 4, 5, 6
 
@@ -79,6 +80,8 @@ def lib() -> ctypes.CDLL:
     L.ncclAllGather.argtypes = [vp, vp, sz, i, vp, vp]
     L.ncclAllToAll.argtypes = [vp, vp, sz, i, vp, vp]
     L.ncclCustomCollective.argtypes = [vp, vp, sz, i, i, vp, vp]
+    L.ncclRedOpCreatePreMulSum.argtypes = [ctypes.POINTER(i), vp, i, i, vp]
+    L.ncclRedOpDestroy.argtypes = [i, vp]
     L.ncclGroupStart.argtypes = []
     L.ncclGroupEnd.argtypes = []
     L.mscclAmdAlgoJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
@@ -225,6 +228,24 @@ class Comm:
         _check(lib().mscclAmdTraceRead(self.handle, buf.ctypes.data, buf.nbytes, ctypes.byref(slots),
                                        ctypes.byref(events)), "mscclAmdTraceRead")
         return buf.reshape(slots.value, events.value)
+
+    # ---- user reduction ops (nccl.h.in:153-174) -----------------------------------------------
+    def create_premulsum(self, scalar, dtype: int, residence: int = 1) -> int:
+        """ncclRedOpCreatePreMulSum.  residence 1 (ncclScalarHostImmediate): `scalar` is bytes of
+        the element type (read now); 0 (ncclScalarDevice): `scalar` is a device address read by
+        every later kernel."""
+        op = ctypes.c_int()
+        if residence == 1:
+            buf = ctypes.create_string_buffer(bytes(scalar), 8)
+            ptr = ctypes.cast(buf, ctypes.c_void_p)
+        else:
+            ptr = ctypes.c_void_p(scalar)
+        _check(lib().ncclRedOpCreatePreMulSum(ctypes.byref(op), ptr, dtype, residence, self.handle),
+               "ncclRedOpCreatePreMulSum")
+        return op.value
+
+    def destroy_op(self, op: int) -> None:
+        _check(lib().ncclRedOpDestroy(op, self.handle), "ncclRedOpDestroy")
 
     # ---- collectives (pointers are device addresses, stream a hipStream_t or 0) ------------
     def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int = SUM, stream: int = 0) -> None:

@@ -40,6 +40,9 @@ enum OpType : uint8_t {
   kCopySend = 9  // ring AllGather out of place (directCopySend, all_gather.h:59); never from XML
 };
 
+// Device reduction ops (ncclDevRedOp_t, devcomm.h): Sum, Prod, Max, Min, PreMulSum, SumPostDiv
+enum DevRedOp : int { kDevSum = 0, kDevProd = 1, kDevMax = 2, kDevMin = 3, kDevPreMulSum = 4, kDevSumPostDiv = 5 };
+
 // Protocol ids (devcomm.h:27-29)
 enum Proto : int { kProtoLL = 0, kProtoLL128 = 1, kProtoSimple = 2, kNumProtos = 3 };
 

@@ -107,6 +107,17 @@ struct ncclComm {
     int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0;
   } last;
 
+  // user reduction ops (ncclRedOpCreatePreMulSum, enqueue.cc:1529-1580): a free list as in the
+  // reference; op ids are ncclNumOps + index, mangled with the communicator (comm.h:223-235)
+  struct UserRedOp {
+    int freeNext = -1;      // -1 = allocated
+    ncclDataType_t datatype = ncclFloat32;
+    uint64_t scalarArg = 0; // scale bits (host immediate) or the scale's device address
+    bool argIsPtr = false;
+  };
+  std::vector<UserRedOp> userRedOps;
+  int userRedOpFreeHead = 0;
+
   hipStream_t userStream = nullptr;
   bool userStreamSet = false;
   hipEvent_t doneEvent = nullptr;

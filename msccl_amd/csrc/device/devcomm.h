@@ -15,6 +15,7 @@
 //     produced are the same as with one workgroup (the split is by element, every element
 //     keeps its operations and their order).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace msccl {
@@ -173,7 +174,8 @@ struct RankWork {
   uint32_t llFlagMask, llCleanMask;
   struct TraceEvent* trace;
   int32_t traceEvents;
-  int32_t pad1;
+  int32_t redOpArgIsPtr;        // redOpArg is a device address of the scalar (ncclScalarDevice)
+  uint64_t redOpArg;            // PreMulSum scale bits / SumPostDiv divisor (ncclDevRedOpFull::scalarArg)
 };
 
 struct LaunchArgs {
@@ -187,6 +189,8 @@ enum : uint32_t { kDevOk = 0, kDevTimeout = 1, kDevAbort = 2, kDevBadOp = 3 };
 
 // Host-side kernel dispatch (kernels.hip)
 typedef int (*LaunchFn)(const LaunchArgs& args, int gridBlocks, void* stream);
+typedef int (*OneRankFn)(const void* src, void* dst, size_t n, uint64_t arg, int argIsPtr, void* stream);
+OneRankFn getOneRankFn(int dtype);
 constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = resident workgroups per CU
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
 

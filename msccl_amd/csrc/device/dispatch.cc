@@ -1,15 +1,31 @@
-// ncclDataType_t x ncclRedOp_t x protocol -> kernel launcher
+// ncclDataType_t x device reduction op x protocol -> kernel launcher
 #include "devcomm.h"
 
 namespace msccl {
-extern LaunchFn gLaunch_i8[4][3], gLaunch_u8[4][3], gLaunch_i32[4][3], gLaunch_u32[4][3], gLaunch_i64[4][3],
-    gLaunch_u64[4][3], gLaunch_f16[4][3], gLaunch_f32[4][3], gLaunch_f64[4][3], gLaunch_bf16[4][3];
+#define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern OneRankFn N##_one;
+MSCCL_DECL(gLaunch_i8)
+MSCCL_DECL(gLaunch_u8)
+MSCCL_DECL(gLaunch_i32)
+MSCCL_DECL(gLaunch_u32)
+MSCCL_DECL(gLaunch_i64)
+MSCCL_DECL(gLaunch_u64)
+MSCCL_DECL(gLaunch_f16)
+MSCCL_DECL(gLaunch_f32)
+MSCCL_DECL(gLaunch_f64)
+MSCCL_DECL(gLaunch_bf16)
 
-LaunchFn getLaunchFn(int dtype, int redop, int proto) {
-  if (redop < 0 || redop > 3 || proto < 0 || proto > 2) return nullptr;
+// devOp: 0..3 Sum/Prod/Max/Min, 4 PreMulSum, 5 SumPostDiv (ncclDevRedOp_t, devcomm.h)
+LaunchFn getLaunchFn(int dtype, int devOp, int proto) {
+  if (devOp < 0 || devOp > 5 || proto < 0 || proto > 2) return nullptr;
   LaunchFn(*tabs[10])[3] = {gLaunch_i8, gLaunch_u8, gLaunch_i32, gLaunch_u32, gLaunch_i64,
                             gLaunch_u64, gLaunch_f16, gLaunch_f32, gLaunch_f64, gLaunch_bf16};
   if (dtype < 0 || dtype > 9) return nullptr;
-  return tabs[dtype][redop][proto];
+  return tabs[dtype][devOp][proto];
+}
+
+OneRankFn getOneRankFn(int dtype) {
+  OneRankFn tabs[10] = {gLaunch_i8_one, gLaunch_u8_one, gLaunch_i32_one, gLaunch_u32_one, gLaunch_i64_one,
+                        gLaunch_u64_one, gLaunch_f16_one, gLaunch_f32_one, gLaunch_f64_one, gLaunch_bf16_one};
+  return dtype >= 0 && dtype <= 9 ? tabs[dtype] : nullptr;
 }
 }  // namespace msccl

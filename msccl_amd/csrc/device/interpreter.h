@@ -73,6 +73,7 @@ struct Shape {
 template <typename T, int OP, int PROTO>
 struct Interp {
   using F = Fn<T, OP>;
+  using PP = PrePost<T, OP>;
   static constexpr int TS = sizeof(T);
   static constexpr int PE = 16 / TS;  // elements per 16-B pack
   static constexpr int U = 4;         // packs per lane per pass (memory-level parallelism)
@@ -93,6 +94,7 @@ struct Interp {
   uint64_t timeoutTicks;  // 0 = wait for ever (DevComm::timeoutTicks)
   uint32_t llFlagMask;    // LL / LL128 flag = (step + 1) & llFlagMask (NCCL_LL_FLAG, devcomm.h:56-63)
   uint32_t llCleanMask;   // cleanup steps: (step & mask) == mask (NCCL_LL_CLEAN_MASK)
+  uint64_t redArg;        // PreMulSum scale bits / SumPostDiv rank count (RankWork::redOpArg)
   int tid;
   int refNthreads;
   TraceEvent* trace;  // this workgroup's trace slot (null = tracing off)
@@ -454,6 +456,11 @@ struct Interp {
 #pragma unroll
         for (int u = 0; u < U; u++)
           if (act[u]) v[u] = loadPack(srs, vec, B[u], s.n);
+        // preOp on data from the user's input (prims_ll.h:280; ring mode only, see PrePost)
+        if constexpr (PP::kPre) {
+#pragma unroll
+          for (int u = 0; u < U; u++) v[u] = PP::pre(v[u], redArg);
+        }
       }
       if (RECV) {
         const void* la[2 * U];
@@ -475,6 +482,12 @@ struct Interp {
           }
           const u32x4 peer = {ln[2 * u].x, ln[2 * u].z, ln[2 * u + 1].x, ln[2 * u + 1].z};
           v[u] = SRC ? F::pack(peer, v[u]) : peer;
+        }
+        // postOp on the final reduction of the ring (rrcs / rrc, all_reduce.h:84,
+        // reduce_scatter.h:65: the only receive-reduce transfers with an output)
+        if constexpr (PP::kPost && SRC && DST) {
+#pragma unroll
+          for (int u = 0; u < U; u++) v[u] = PP::post(v[u], redArg);
         }
       }
       if (SEND) {
@@ -609,6 +622,10 @@ struct Interp {
 #pragma unroll
           for (int u = 0; u < U; u++)
             if (act[u]) v[u] = loadPack(srs, vec, B[u], s.n);
+          if constexpr (PP::kPre) {  // PreOpN = 1: the local input (prims_simple.h:209-211)
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = PP::pre(v[u], redArg);
+          }
         }
         if (RECV) {
 #pragma unroll
@@ -616,6 +633,10 @@ struct Interp {
             if (act[u]) peer[u] = ld16<kAuxFifo>(rrs, (uint32_t)(base + u * kNT - s0) * 16);
 #pragma unroll
           for (int u = 0; u < U; u++) v[u] = SRC ? F::pack(v[u], peer[u]) : peer[u];
+          if constexpr (PP::kPost && SRC && DST) {
+#pragma unroll
+            for (int u = 0; u < U; u++) v[u] = PP::post(v[u], redArg);
+          }
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -729,6 +750,14 @@ struct Interp {
     refNthreads = w.refNthreads;
     t0 = __builtin_amdgcn_s_memrealtime();
     timeoutTicks = w.timeoutTicks;
+    redArg = w.redOpArg;
+    if (w.redOpArgIsPtr) {  // ncclScalarDevice: the scale lives in device memory (enqueue.cc:1549-1557)
+      T x;
+      __builtin_memcpy(&x, (const void*)w.redOpArg, sizeof(T));
+      redArg = 0;
+      __builtin_memcpy(&redArg, &x, sizeof(T));
+      redArg = uni(redArg);
+    }
     llFlagMask = w.llFlagMask;
     llCleanMask = w.llCleanMask;
     const int split = w.split;

@@ -19,11 +19,42 @@ int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-#define MSCCL_DEFINE_TABLE(NAME, T)                                                                 \
-  LaunchFn NAME[4][3] = {                                                                           \
-      {launchKernel<T, kSum, pLL>, launchKernel<T, kSum, pLL128>, launchKernel<T, kSum, pSimple>},             \
-      {launchKernel<T, kProd, pLL>, launchKernel<T, kProd, pLL128>, launchKernel<T, kProd, pSimple>},           \
-      {launchKernel<T, kMax, pLL>, launchKernel<T, kMax, pLL128>, launchKernel<T, kMax, pSimple>},             \
-      {launchKernel<T, kMin, pLL>, launchKernel<T, kMin, pLL128>, launchKernel<T, kMin, pSimple>}};
+// nRanks == 1 with a user PreMulSum op: dst = src * scale (the reference's oneRankReduce,
+// onerank_reduce.cu:12-44: ReduceOrCopyMulti with the preOp applied, postOp identity).
+template <typename T>
+__global__ void __launch_bounds__(256) oneRankScaleKernel(const T* src, T* dst, size_t n, uint64_t arg, int argIsPtr) {
+  if (argIsPtr) {
+    T x;
+    __builtin_memcpy(&x, (const void*)arg, sizeof(T));
+    arg = 0;
+    __builtin_memcpy(&arg, &x, sizeof(T));
+  }
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    dst[i] = scaleElem<T>(src[i], arg);
+}
+
+template <typename T>
+int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int argIsPtr, void* stream) {
+  const size_t blocks = n == 0 ? 1 : (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
+  hipLaunchKernelGGL((oneRankScaleKernel<T>), dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, (const T*)src,
+                     (T*)dst, n, arg, argIsPtr);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
+// [op][protocol]: Sum, Prod, Max, Min, PreMulSum, SumPostDiv x LL, LL128, Simple.  PreMulSum and
+// SumPostDiv only run in the ring fallback (LL or Simple); SumPostDiv exists for integer types.
+#define MSCCL_OPS_0_3(T)                                                                                   \
+  {launchKernel<T, kSum, pLL>, launchKernel<T, kSum, pLL128>, launchKernel<T, kSum, pSimple>},             \
+      {launchKernel<T, kProd, pLL>, launchKernel<T, kProd, pLL128>, launchKernel<T, kProd, pSimple>},      \
+      {launchKernel<T, kMax, pLL>, launchKernel<T, kMax, pLL128>, launchKernel<T, kMax, pSimple>},         \
+      {launchKernel<T, kMin, pLL>, launchKernel<T, kMin, pLL128>, launchKernel<T, kMin, pSimple>},         \
+      {launchKernel<T, kPreMulSum, pLL>, nullptr, launchKernel<T, kPreMulSum, pSimple>}
+#define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
+  LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \
+                         {launchKernel<T, kSumPostDiv, pLL>, nullptr, launchKernel<T, kSumPostDiv, pSimple>}}; \
+  OneRankFn NAME##_one = launchOneRankScale<T>;
+#define MSCCL_DEFINE_TABLE_FP(NAME, T)                                                                     \
+  LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T), {nullptr, nullptr, nullptr}};                                   \
+  OneRankFn NAME##_one = launchOneRankScale<T>;
 
 }  // namespace msccl

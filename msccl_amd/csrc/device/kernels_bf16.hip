@@ -1,2 +1,2 @@
 #include "kernels.h"
-namespace msccl { MSCCL_DEFINE_TABLE(gLaunch_bf16, Bf16) }
+namespace msccl { MSCCL_DEFINE_TABLE_FP(gLaunch_bf16, Bf16) }

@@ -1,2 +1,2 @@
 #include "kernels.h"
-namespace msccl { MSCCL_DEFINE_TABLE(gLaunch_f16, _Float16) }
+namespace msccl { MSCCL_DEFINE_TABLE_FP(gLaunch_f16, _Float16) }

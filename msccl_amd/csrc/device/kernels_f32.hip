@@ -1,2 +1,2 @@
 #include "kernels.h"
-namespace msccl { MSCCL_DEFINE_TABLE(gLaunch_f32, float) }
+namespace msccl { MSCCL_DEFINE_TABLE_FP(gLaunch_f32, float) }

@@ -42,9 +42,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t makeRsrc(const void* p) {
 // interpreter state stays out of the vector register budget of the hot loops.
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// (readfirstlane returns int: both halves go through uint32_t, or a low half with bit 31 set
+// would sign-extend over the high half)
 __device__ __forceinline__ uint64_t uni(uint64_t x) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-         __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+  return ((uint64_t)hi << 32) | lo;
 }
 
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
@@ -174,7 +177,12 @@ __device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)
 
 // ---------------------------------------------------------------------------------------------
 // Elementwise functors.  fn(x, y) keeps the reference's operand order.
-enum RedOp { kSum = 0, kProd = 1, kMax = 2, kMin = 3 };
+// kPreMulSum / kSumPostDiv are the reference's device ops for ncclAvg and user PreMulSum ops
+// (reduce_kernel.h:498-560, enqueue.cc:1388-1454): a sum whose inputs are scaled before (preOp)
+// or whose result is divided after (postOp).  They only run in the ring fallback, as in the
+// reference, where MSCCL admits Sum/Prod/Max/Min only (tuning.cc:345).
+enum RedOp { kSum = 0, kProd = 1, kMax = 2, kMin = 3, kPreMulSum = 4, kSumPostDiv = 5 };
+constexpr int baseOp(int op) { return op >= kPreMulSum ? kSum : op; }
 
 template <typename T> struct IsHalf { static constexpr bool v = false; };
 template <> struct IsHalf<_Float16> { static constexpr bool v = true; };
@@ -185,9 +193,10 @@ template <typename T, int OP>
 struct Fn {
   __device__ __forceinline__ static T elem(T x, T y) {
     using U = typename std::make_unsigned<T>::type;  // two's-complement wrap, no signed-overflow UB
-    if constexpr (OP == kSum) return (T)(U)((U)x + (U)y);
-    else if constexpr (OP == kProd) return (T)(U)((U)x * (U)y);
-    else if constexpr (OP == kMax) return (x < y) ? y : x;
+    constexpr int B = baseOp(OP);
+    if constexpr (B == kSum) return (T)(U)((U)x + (U)y);
+    else if constexpr (B == kProd) return (T)(U)((U)x * (U)y);
+    else if constexpr (B == kMax) return (x < y) ? y : x;
     else return (x < y) ? x : y;
   }
   __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
@@ -206,9 +215,10 @@ struct Fn {
 template <int OP>
 struct Fn<float, OP> {
   __device__ __forceinline__ static float elem(float x, float y) {
-    if constexpr (OP == kSum) return x + y;
-    else if constexpr (OP == kProd) return x * y;
-    else if constexpr (OP == kMax) return __builtin_fmaxf(x, y);
+    constexpr int B = baseOp(OP);
+    if constexpr (B == kSum) return x + y;
+    else if constexpr (B == kProd) return x * y;
+    else if constexpr (B == kMax) return __builtin_fmaxf(x, y);
     else return __builtin_fminf(x, y);
   }
   __device__ __forceinline__ static uint32_t e1(uint32_t a, uint32_t b) {
@@ -222,9 +232,10 @@ struct Fn<float, OP> {
 template <int OP>
 struct Fn<double, OP> {
   __device__ __forceinline__ static double elem(double x, double y) {
-    if constexpr (OP == kSum) return x + y;
-    else if constexpr (OP == kProd) return x * y;
-    else if constexpr (OP == kMax) return __builtin_fmax(x, y);
+    constexpr int B = baseOp(OP);
+    if constexpr (B == kSum) return x + y;
+    else if constexpr (B == kProd) return x * y;
+    else if constexpr (B == kMax) return __builtin_fmax(x, y);
     else return __builtin_fmin(x, y);
   }
   __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
@@ -242,17 +253,18 @@ struct Fn<double, OP> {
 template <int OP>
 struct Fn<_Float16, OP> {
   __device__ __forceinline__ static f16x2 op2(f16x2 x, f16x2 y) {
-    if constexpr (OP == kSum) {
+    constexpr int B = baseOp(OP);
+    if constexpr (B == kSum) {
       f16x2 r = x + y;  // v_pk_add_f16, RNE
       r = __builtin_elementwise_max(r, (f16x2){(_Float16)-65504.0f, (_Float16)-65504.0f});
       r = __builtin_elementwise_min(r, (f16x2){(_Float16)65504.0f, (_Float16)65504.0f});
       return r;
-    } else if constexpr (OP == kProd) {
+    } else if constexpr (B == kProd) {
       return x * y;
     } else {
       f32x2 fx = __builtin_convertvector(x, f32x2), fy = __builtin_convertvector(y, f32x2);
       f32x2 m;
-      if constexpr (OP == kMax) m = (f32x2){__builtin_fmaxf(fx[0], fy[0]), __builtin_fmaxf(fx[1], fy[1])};
+      if constexpr (B == kMax) m = (f32x2){__builtin_fmaxf(fx[0], fy[0]), __builtin_fmaxf(fx[1], fy[1])};
       else m = (f32x2){__builtin_fminf(fx[0], fy[0]), __builtin_fminf(fx[1], fy[1])};
       return __builtin_convertvector(m, f16x2);
     }
@@ -274,9 +286,10 @@ struct Fn<Bf16, OP> {
   __device__ __forceinline__ static bf16x2 op2(bf16x2 x, bf16x2 y) {
     f32x2 fx = __builtin_convertvector(x, f32x2), fy = __builtin_convertvector(y, f32x2);
     f32x2 r;
-    if constexpr (OP == kSum) r = fx + fy;
-    else if constexpr (OP == kProd) r = fx * fy;
-    else if constexpr (OP == kMax) r = (f32x2){__builtin_fmaxf(fx[0], fy[0]), __builtin_fmaxf(fx[1], fy[1])};
+    constexpr int B = baseOp(OP);
+    if constexpr (B == kSum) r = fx + fy;
+    else if constexpr (B == kProd) r = fx * fy;
+    else if constexpr (B == kMax) r = (f32x2){__builtin_fmaxf(fx[0], fy[0]), __builtin_fmaxf(fx[1], fy[1])};
     else r = (f32x2){__builtin_fminf(fx[0], fy[0]), __builtin_fminf(fx[1], fy[1])};
     return __builtin_convertvector(r, bf16x2);  // v_cvt_pk_bf16_f32 (RNE)
   }
@@ -292,6 +305,69 @@ struct Fn<Bf16, OP> {
   }
   __device__ __forceinline__ static u32x4 pack(u32x4 a, u32x4 b) {
     return (u32x4){e1(a.x, b.x), e1(a.y, b.y), e1(a.z, b.z), e1(a.w, b.w)};
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// preOp / postOp of kPreMulSum and kSumPostDiv (reduce_kernel.h:498-687); identity otherwise.
+// The scalar travels as the reference's 64-bit opArg: the scale's bits in the low bytes
+// (PreMulSum) or the rank count (SumPostDiv).
+template <typename T, int OP>
+struct PrePost {
+  static constexpr bool kPre = false, kPost = false;
+  __device__ __forceinline__ static u32x4 pre(u32x4 v, uint64_t) { return v; }
+  __device__ __forceinline__ static u32x4 post(u32x4 v, uint64_t) { return v; }
+};
+
+template <typename T>
+__device__ __forceinline__ T scaleElem(T x, uint64_t arg) {
+  T s;
+  __builtin_memcpy(&s, &arg, sizeof(T));
+  if constexpr (std::is_same<T, float>::value || std::is_same<T, double>::value) {
+    return x * s;
+  } else if constexpr (std::is_same<T, _Float16>::value) {
+    return x * s;                                        // v_mul_f16 / __hmul: one rounding
+  } else if constexpr (std::is_same<T, Bf16>::value) {
+    uint32_t fx = (uint32_t)x.bits << 16, fs = (uint32_t)s.bits << 16;
+    const float p = __builtin_bit_cast(float, fx) * __builtin_bit_cast(float, fs);  // exact in fp32
+    const bf16x2 r = __builtin_convertvector((f32x2){p, p}, bf16x2);              // RNE to bf16
+    Bf16 o;
+    o.bits = (uint16_t)__builtin_bit_cast(uint32_t, r);
+    return o;
+  } else {
+    using U = typename std::make_unsigned<T>::type;     // FuncPreMulSum<int>: x * scale, wrapping
+    return (T)(U)((U)x * (U)s);
+  }
+}
+
+template <typename T>
+struct PrePost<T, kPreMulSum> {
+  static constexpr bool kPre = true, kPost = false;
+  __device__ __forceinline__ static u32x4 pre(u32x4 v, uint64_t arg) {
+    constexpr int N = 16 / sizeof(T);
+    T x[N];
+    __builtin_memcpy(x, &v, 16);
+#pragma unroll
+    for (int i = 0; i < N; i++) x[i] = scaleElem<T>(x[i], arg);
+    __builtin_memcpy(&v, x, 16);
+    return v;
+  }
+  __device__ __forceinline__ static u32x4 post(u32x4 v, uint64_t) { return v; }
+};
+
+template <typename T>
+struct PrePost<T, kSumPostDiv> {  // integral types only (reduce_kernel.h:498-517)
+  static constexpr bool kPre = false, kPost = true;
+  __device__ __forceinline__ static u32x4 pre(u32x4 v, uint64_t) { return v; }
+  __device__ __forceinline__ static u32x4 post(u32x4 v, uint64_t arg) {
+    constexpr int N = 16 / sizeof(T);
+    const int n = (int)arg;
+    T x[N];
+    __builtin_memcpy(x, &v, 16);
+#pragma unroll
+    for (int i = 0; i < N; i++) x[i] = T(x[i] / n);       // T(x/n) with int n, as the reference
+    __builtin_memcpy(&v, x, 16);
+    return v;
   }
 };
 

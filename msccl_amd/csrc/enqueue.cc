@@ -47,6 +47,7 @@ struct Planned {
   CollOp op;
   Plan plan;
   bool memcpyOnly = false;
+  bool oneRankScale = false;
   size_t copyBytes = 0;
   bool noop = false;
   bool inPlace = false;
@@ -58,6 +59,12 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   int ts = refTypeSize(op.dtype);
   if (op.count == 0) { out->noop = true; return ncclSuccess; }
   if (comm->nRanks == 1) {
+    if ((int)op.op >= (int)ncclNumOps) {
+      // a user PreMulSum op still scales a single rank's data: the reference's oneRankReduce
+      // (enqueue.cc:811-816 skips only built-in ops, onerank_reduce.cu:12-44)
+      out->oneRankScale = true;
+      return ncclSuccess;
+    }
     // enqueue.cc:811-816: one rank = device-to-device copy (or nothing when in place)
     out->memcpyOnly = true;
     out->copyBytes = op.count * (size_t)ts;
@@ -68,7 +75,7 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   c.coll = op.coll;
   c.count = op.count;
   c.dtype = op.dtype;
-  c.redop = op.op;
+  c.redop = op.devOp;
   c.nRanks = comm->nRanks;
   c.rank = comm->rank;
   c.inPlace = inPlaceOf(op.coll, op.sendbuff, op.recvbuff, op.count, op.dtype, comm->rank);
@@ -142,6 +149,8 @@ RankWork makeRingWork(Planned& p) {
   w.llCleanMask = comm->llCleanMask;
   w.trace = comm->dTrace;
   w.traceEvents = comm->traceEvents;
+  w.redOpArg = p.op.redArg;
+  w.redOpArgIsPtr = p.op.redArgIsPtr;
   w.flags = comm->dFlags;
   w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
   w.maxSplit = comm->maxSplit;
@@ -181,6 +190,8 @@ RankWork makeWork(Planned& p) {
   w.llCleanMask = comm->llCleanMask;
   w.trace = comm->dTrace;
   w.traceEvents = comm->traceEvents;
+  w.redOpArg = p.op.redArg;
+  w.redOpArgIsPtr = p.op.redArgIsPtr;
   w.flags = comm->dFlags;
   w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
   w.maxSplit = comm->maxSplit;
@@ -258,8 +269,8 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
     }
   }
   const Planned& p0 = *ps[0];
-  LaunchFn fn = getLaunchFn(p0.plan.dtype, p0.op.op, p0.plan.proto);
-  if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, (int)p0.op.op, p0.plan.proto); return ncclInvalidArgument; }
+  LaunchFn fn = getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
+  if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {
     // Every workgroup of the launch may spin on every other one (FIFO credits, dependency
     // flags), so all of them must be resident at once: refuse what the GPU cannot hold instead
@@ -335,7 +346,15 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
         }
         continue;
       }
-      launches[std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, (int)p.op.op, p.plan.proto)].push_back(&p);
+      if (p.oneRankScale) {
+        OneRankFn f = getOneRankFn((int)p.op.dtype);
+        if (!f || f(p.op.sendbuff, p.op.recvbuff, p.op.count, p.op.redArg, p.op.redArgIsPtr, (void*)p.op.stream) != 0) {
+          res = ncclUnhandledCudaError;
+          break;
+        }
+        continue;
+      }
+      launches[std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto)].push_back(&p);
     }
     for (auto& kv : launches) {
       if (res != ncclSuccess) break;
@@ -361,6 +380,107 @@ using namespace msccl;
 
 namespace {
 
+// IEEE binary16 of a float, round to nearest even (__float2half); the host compiler has no
+// _Float16.  Normal and subnormal results, overflow to infinity, NaN kept quiet.
+uint16_t floatToHalfRne(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0));
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds to >= 65520: infinity
+  if (ax < 0x38800000u) {                                      // subnormal or zero half
+    if (ax < 0x33000000u) return (uint16_t)sign;               // at most half the smallest subnormal
+    const uint32_t m = (ax & 0x7fffffu) | 0x800000u;           // value = m * 2^(e - 150)
+    const int s = 126 - (int)(ax >> 23);                       // half subnormal = value * 2^24 = m >> s
+    uint32_t h = m >> s;
+    const uint32_t rem = m & ((1u << s) - 1), halfway = 1u << (s - 1);
+    if (rem > halfway || (rem == halfway && (h & 1u))) h++;    // may carry into the smallest normal
+    return (uint16_t)(sign | h);
+  }
+  const uint32_t e = (ax >> 23) - 112, m = ax & 0x7fffffu;
+  uint32_t h = (e << 10) | (m >> 13);
+  const uint32_t rem = m & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+  return (uint16_t)(sign | h);
+}
+
+// ncclUserRedOpMangle (comm.h:223-235): user op ids are ncclNumOps + index, xor-ed with a hash
+// of the communicator so an op from another communicator is rejected; an involution.
+ncclRedOp_t userRedOpMangle(const ncclComm* comm, ncclRedOp_t op) {
+  if ((int)op < (int)ncclNumOps) return op;
+  uint64_t h = reinterpret_cast<uint64_t>(comm);
+  h ^= h >> 32;
+  h *= 0x9e3779b97f4a7c13ull;
+  h >>= 32;
+  h &= (uint64_t)ncclMaxRedOp;
+  const int op1 = (int)h ^ (int)op;
+  return op1 < (int)ncclNumOps ? op : (ncclRedOp_t)op1;
+}
+
+// hostToDevRedOp (enqueue.cc:1388-1454): the device operation of a call.  ncclAvg is a sum of
+// inputs pre-multiplied by 1/nRanks (rounded to the element type) for floating types, and a
+// sum divided by nRanks afterwards for integer types.
+ncclResult_t hostToDevRedOp(ncclComm* comm, ncclRedOp_t op, ncclDataType_t dt, CollOp* o, const char* name) {
+  o->redArg = 0;
+  o->redArgIsPtr = 0;
+  if ((int)op < (int)ncclAvg) {
+    o->devOp = (int)op;
+    return ncclSuccess;
+  }
+  if (op == ncclAvg) {
+    const int n = comm->nRanks;
+    switch (dt) {
+      case ncclInt8: case ncclUint8: case ncclInt32: case ncclUint32: case ncclInt64: case ncclUint64:
+        o->devOp = kDevSumPostDiv;
+        o->redArg = (uint64_t)n;
+        break;
+      case ncclFloat16: {
+        const uint16_t s = floatToHalfRne((float)(1.0 / n));  // __float2half(float(1.0/n))
+        memcpy(&o->redArg, &s, 2);
+        o->devOp = kDevPreMulSum;
+        break;
+      }
+      case ncclBfloat16: {
+        const float f = (float)(1.0 / n);              // __float2bfloat16(float(1.0/n)): RNE
+        uint32_t u;
+        memcpy(&u, &f, 4);
+        const uint16_t b = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+        memcpy(&o->redArg, &b, 2);
+        o->devOp = kDevPreMulSum;
+        break;
+      }
+      case ncclFloat32: {
+        const float f = (float)(1.0 / n);
+        memcpy(&o->redArg, &f, 4);
+        o->devOp = kDevPreMulSum;
+        break;
+      }
+      default: {  // ncclFloat64
+        const double d = 1.0 / n;
+        memcpy(&o->redArg, &d, 8);
+        o->devOp = kDevPreMulSum;
+        break;
+      }
+    }
+    return ncclSuccess;
+  }
+  const int ix = (int)userRedOpMangle(comm, op) - (int)ncclNumOps;
+  if (ix < 0 || ix >= (int)comm->userRedOps.size() || comm->userRedOps[ix].freeNext != -1) {
+    WARN("%s : reduction operation %d unknown to this communicator", name, (int)op);
+    return ncclInvalidArgument;
+  }
+  const ncclComm::UserRedOp& u = comm->userRedOps[ix];
+  if (u.datatype != dt) {
+    WARN("Data type supplied to user-created ncclRedOp_t does not match type given to reduction operation");
+    return ncclInvalidArgument;
+  }
+  o->devOp = kDevPreMulSum;
+  o->redArg = u.scalarArg;
+  o->redArgIsPtr = u.argIsPtr ? 1 : 0;
+  return ncclSuccess;
+}
+
 ncclResult_t enqueue(ncclComm* comm, int coll, const void* sendbuff, void* recvbuff, size_t count,
                      ncclDataType_t dtype, ncclRedOp_t op, hipStream_t stream, int customAlgo, const char* name) {
   if (!commValid(comm)) { WARN("%s : invalid communicator", name); return ncclInvalidArgument; }
@@ -373,9 +493,9 @@ ncclResult_t enqueue(ncclComm* comm, int coll, const void* sendbuff, void* recvb
   }
   if ((int)dtype < 0 || (int)dtype >= ncclNumTypes) { WARN("%s : invalid type %d", name, (int)dtype); return ncclInvalidArgument; }
   if ((int)op < 0 || (int)op > (int)ncclMaxRedOp) { WARN("%s : invalid reduction operation %d", name, (int)op); return ncclInvalidArgument; }
-  if ((int)op >= (int)ncclNumOps) { WARN("%s : reduction operation %d unknown to this communicator", name, (int)op); return ncclInvalidArgument; }
   if (count > 0 && (sendbuff == nullptr || recvbuff == nullptr)) { WARN("%s : buffer argument is NULL", name); return ncclInvalidArgument; }
   CollOp o{comm, coll, sendbuff, recvbuff, count, dtype, op, stream, customAlgo};
+  NCCLCHECK(hostToDevRedOp(comm, op, dtype, &o, name));
   if (groupActive()) {
     groupAddOp(o);
     return ncclSuccess;
@@ -412,6 +532,53 @@ ncclResult_t ncclCustomCollective(const void* sendbuff, void* recvbuff, size_t c
                                   int mscclAlgorithmIndex, ncclComm_t comm, hipStream_t stream) {
   return enqueue(comm, kCustom, sendbuff, recvbuff, count, datatype, ncclSum, stream, mscclAlgorithmIndex,
                  "CustomCollective");
+}
+
+ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,
+                                      ncclScalarResidence_t residence, ncclComm_t comm) {
+  if (!commValid(comm) || op == nullptr || scalar == nullptr) return ncclInvalidArgument;
+  if ((int)datatype < 0 || (int)datatype >= ncclNumTypes) return ncclInvalidArgument;
+  if (comm->userRedOpFreeHead == (int)comm->userRedOps.size()) {  // grow the free list
+    const int cap = std::max<int>(4, 2 * (int)comm->userRedOps.size());
+    const int old = (int)comm->userRedOps.size();
+    comm->userRedOps.resize(cap);
+    for (int i = old; i < cap; i++) comm->userRedOps[i].freeNext = i + 1;
+  }
+  const int ix = comm->userRedOpFreeHead;
+  ncclComm::UserRedOp& u = comm->userRedOps[ix];
+  comm->userRedOpFreeHead = u.freeNext;
+  u.freeNext = -1;
+  u.datatype = datatype;
+  u.scalarArg = 0;
+  if (residence == ncclScalarHostImmediate) {
+    u.argIsPtr = false;
+    memcpy(&u.scalarArg, scalar, (size_t)refTypeSize((int)datatype));
+  } else {
+    u.argIsPtr = true;
+    u.scalarArg = reinterpret_cast<uint64_t>(scalar);
+  }
+  *op = userRedOpMangle(comm, (ncclRedOp_t)((int)ncclNumOps + ix));
+  return ncclSuccess;
+}
+
+ncclResult_t ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm) {
+  if (0 <= (int)op && (int)op < (int)ncclNumOps) {
+    WARN("ncclRedOpDestroy : operator is a NCCL builtin.");
+    return ncclInvalidArgument;
+  }
+  if ((int)op < 0 || (int)ncclMaxRedOp < (int)op) {
+    WARN("ncclRedOpDestroy :  operator is garbage.");
+    return ncclInvalidArgument;
+  }
+  if (!commValid(comm)) return ncclInvalidArgument;
+  const int ix = (int)userRedOpMangle(comm, op) - (int)ncclNumOps;
+  if (ix < 0 || ix >= (int)comm->userRedOps.size() || comm->userRedOps[ix].freeNext != -1) {
+    WARN("ncclRedOpDestroy : operator unknown to this communicator.");
+    return ncclInvalidArgument;
+  }
+  comm->userRedOps[ix].freeNext = comm->userRedOpFreeHead;
+  comm->userRedOpFreeHead = ix;
+  return ncclSuccess;
 }
 
 ncclResult_t ncclGroupStart() {

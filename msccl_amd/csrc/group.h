@@ -19,6 +19,11 @@ struct CollOp {
   ncclRedOp_t op;
   hipStream_t stream;
   int customAlgo;
+  // device reduction (hostToDevRedOp, enqueue.cc:1388-1454): 0..3 Sum/Prod/Max/Min,
+  // 4 PreMulSum (scale bits or scale address in redArg), 5 SumPostDiv (divisor in redArg)
+  int devOp = 0;
+  uint64_t redArg = 0;
+  int redArgIsPtr = 0;
 };
 
 bool groupActive();

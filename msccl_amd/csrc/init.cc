@@ -489,13 +489,6 @@ ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
 
 const char* ncclGetLastError(ncclComm_t comm) { return lastError(); }
 
-ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,
-                                      ncclScalarResidence_t residence, ncclComm_t comm) {
-  WARN("ncclRedOpCreatePreMulSum: PreMulSum is not an MSCCL-eligible operator (tuning.cc:345) and the "
-       "ring/tree fallback is not built");
-  return ncclInvalidUsage;
-}
 
-ncclResult_t ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm) { return ncclInvalidArgument; }
 
 }  // extern "C"

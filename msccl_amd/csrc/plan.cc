@@ -201,7 +201,8 @@ int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverri
 int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   *p = Plan();
   p->algoIndex = -1;
-  if (!(c.redop == 0 || c.redop == 1 || c.redop == 2 || c.redop == 3)) return 5;
+  if (c.redop < 0 || c.redop > kDevSumPostDiv) return 5;
+  if (c.redop == kDevSumPostDiv && !(c.dtype <= 5)) return 5;  // SumPostDiv is for integer types
   if (c.coll == kAllReduce) p->ringColl = kRingAllReduce;
   else if (c.coll == kReduceScatter) p->ringColl = kRingReduceScatter;
   else if (c.coll == kAllGather) p->ringColl = kRingAllGather;

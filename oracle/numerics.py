@@ -11,6 +11,13 @@ Restates /root/reference/src/collectives/device/reduce_kernel.h as numpy operati
   FuncMax/Min<bf16> (sm_80)           reduce_kernel.h:390-440   __hmax2/__hmin2 (NaN -> other)
   FuncMax/Min<float>/<double>         reduce_kernel.h:442-470   fmaxf/fminf, fmax/fmin
   integer types                        reduce_kernel.h:64-230    two's-complement wrap-around
+  FuncPreMulSum / FuncSumPostDiv      reduce_kernel.h:498-687   a sum whose inputs are scaled first
+                                                                 (x*scale, one rounding: __hmul/__hmul2/
+                                                                 fp32/fp64 multiply, integer wrap) or whose
+                                                                 result is divided after (T(x/n), C
+                                                                 truncation; integer types only)
+  ncclAvg                             enqueue.cc:1388-1454      PreMulSum by 1/n rounded to the type
+                                                                 (floats), SumPostDiv by n (integers)
 fp16/bf16 sums are formed in fp32 and rounded once to the 16-bit format; for a sum or product
 of two p-bit values an fp32 (24-bit) intermediate satisfies q >= 2p+2, so the double rounding is
 innocuous and the result equals the correctly rounded value the reference's __hadd2/__hmul2 give.
@@ -21,7 +28,8 @@ from __future__ import annotations
 
 import numpy as np
 
-SUM, PROD, MAX, MIN = 0, 1, 2, 3
+SUM, PROD, MAX, MIN, PREMULSUM, SUMPOSTDIV = 0, 1, 2, 3, 4, 5
+AVG = 4  # ncclAvg (host op); lowered by avg_op() to PREMULSUM or SUMPOSTDIV
 
 # ncclDataType_t -> (numpy storage dtype, element size, kind)
 DTYPES = {
@@ -63,6 +71,8 @@ def _clamp_f16(r: np.ndarray) -> np.ndarray:
 
 def apply(op: int, dt: int, x: np.ndarray, y: np.ndarray) -> np.ndarray:
     """fn(x, y) with the reference's operand order (x is the first functor argument)."""
+    if op in (PREMULSUM, SUMPOSTDIV):   # both reduce with FuncSum (reduce_kernel.h:498-520)
+        op = SUM
     kind = DTYPES[dt][2]
     with np.errstate(all="ignore"):
         if kind == "int":
@@ -99,6 +109,57 @@ def apply(op: int, dt: int, x: np.ndarray, y: np.ndarray) -> np.ndarray:
         if op == MAX:
             return f32_to_bf16(np.fmax(fx, fy))
         return f32_to_bf16(np.fmin(fx, fy))
+
+
+def scalar_bits(dt: int, value) -> int:
+    """The 64-bit opArg of a PreMulSum scale: the value's bits in the element type, low bytes."""
+    a = from_float(dt, np.array([value], dtype=np.float64)) if DTYPES[dt][2] != "int" else \
+        np.array([value]).astype(storage(dt))
+    return int.from_bytes(np.ascontiguousarray(a).tobytes().ljust(8, b"\0"), "little")
+
+
+def avg_op(dt: int, nranks: int):
+    """hostToDevRedOp for ncclAvg (enqueue.cc:1403-1431): (device op, opArg).  The scale is
+    1.0/n rounded through float for f16/bf16/f32 (__float2half(float(1.0/n)) etc.), 1.0/n for f64."""
+    kind = DTYPES[dt][2]
+    if kind == "int":
+        return SUMPOSTDIV, nranks
+    if kind == "f64":
+        return PREMULSUM, scalar_bits(dt, 1.0 / nranks)
+    return PREMULSUM, scalar_bits(dt, float(np.float32(1.0 / nranks)))
+
+
+def _scale_of(dt: int, arg: int):
+    b = int(arg).to_bytes(8, "little")[:type_size(dt)]
+    return np.frombuffer(b, dtype=storage(dt))[0]
+
+
+def pre_op(op: int, dt: int, x: np.ndarray, arg: int) -> np.ndarray:
+    """FuncPreMulSum::preOp: x * scale with one rounding in the element type; identity otherwise."""
+    if op != PREMULSUM:
+        return x
+    kind = DTYPES[dt][2]
+    s = _scale_of(dt, arg)
+    with np.errstate(all="ignore"):
+        if kind == "int":
+            return (x * s).astype(x.dtype)
+        if kind in ("f32", "f64"):
+            return (x * s).astype(x.dtype)
+        if kind == "f16":
+            return (x.astype(np.float32) * np.float32(s)).astype(np.float16)   # exact in fp32, one RNE
+        return f32_to_bf16(bf16_to_f32(x) * bf16_to_f32(np.array([s], np.uint16))[0])
+
+
+def post_op(op: int, dt: int, x: np.ndarray, arg: int) -> np.ndarray:
+    """FuncSumPostDiv::postOp: T(x / n) with C truncation toward zero; identity otherwise."""
+    if op != SUMPOSTDIV:
+        return x
+    n = int(arg)
+    xi = x.astype(np.int64) if x.dtype != np.uint64 else x
+    if x.dtype == np.uint64:
+        return (x // np.uint64(n)).astype(x.dtype)
+    q = np.abs(xi) // n * np.sign(xi)
+    return q.astype(x.dtype)
 
 
 def to_float64(dt: int, a: np.ndarray) -> np.ndarray:

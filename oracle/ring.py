@@ -11,6 +11,9 @@ and the host chunk math:
   nThreads       enqueue.cc:486-523 (LL 512; Simple 512 + one sync warp, 516-517)
 Primitive values: LL recv-reduce fn(peer, local) (prims_ll.h:282-287); Simple fn(local, peer)
 (common_kernel.h:490-555, srcs = [local, peer]).  A primitive with nelem <= 0 moves nothing.
+PreMulSum / SumPostDiv (ncclAvg, user ops): every value loaded from the user's input is scaled
+first (prims_ll.h:280, prims_simple.h:209-211 PreOpN), and the final reduction of AllReduce (rrcs,
+all_reduce.h:84) and ReduceScatter (rrc, reduce_scatter.h:65) applies the postOp.
 
 Where the reference consults its topology search and tuning model (graph/search.cc,
 tuning.cc:77-309, enqueue.cc:486-515), this build decides as follows; ring_params() states it and
@@ -149,7 +152,7 @@ def ops(rp: dict, rank: int, n: int, bid: int):
 
 
 def run(coll: int, count: int, dtype: int, op: int, inputs: Sequence[np.ndarray],
-        outputs: Sequence[Optional[np.ndarray]], in_place: bool):
+        outputs: Sequence[Optional[np.ndarray]], in_place: bool, arg: int = 0):
     """Run the ring fallback on all ranks.  inputs/outputs as oracle/sim.run (element type of the
     call; AllGather buffers may be any type, they are moved as bytes).  For in-place calls pass
     outputs[r]=None except for AllGather, whose output buffer holds the input at rank*count.
@@ -194,13 +197,18 @@ def run(coll: int, count: int, dtype: int, op: int, inputs: Sequence[np.ndarray]
                     outs[r][do:do + ne] = v
                 fifos.setdefault((bid, r, nxt), []).append(v)
             elif kind == "s":
-                fifos.setdefault((bid, r, nxt), []).append(ins[r][so:so + ne].copy())
+                v = ins[r][so:so + ne].copy()
+                if coll != L.ALLGATHER:
+                    v = N.pre_op(op, dt, v, arg)
+                fifos.setdefault((bid, r, nxt), []).append(v)
             elif kind in ("rrs", "rrcs", "rrc"):
-                local = ins[r][so:so + ne].copy()
+                local = N.pre_op(op, dt, ins[r][so:so + ne].copy(), arg)
                 if rp["proto"] == L.PROTO_SIMPLE:
                     v = N.apply(op, dt, local, msg)
                 else:
                     v = N.apply(op, dt, msg, local)
+                if kind in ("rrcs", "rrc"):
+                    v = N.post_op(op, dt, v, arg)
                 if kind in ("rrcs", "rrc"):
                     outs[r][do:do + ne] = v
                 if kind in ("rrs", "rrcs"):

@@ -146,8 +146,10 @@ def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, o
 
 
 def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, in_place: bool = True,
-                      seed: int = 1, mode: str = "uniform", iters: int = 1):
+                      seed: int = 1, mode: str = "uniform", iters: int = 1, user_scale=None):
     """No MSCCL schedule loaded: every call takes the ring fallback (enqueue.cc:461-476).
+    op 4 = ncclAvg.  user_scale=(value, residence): each rank creates a PreMulSum op with that
+    scale (residence 1 host immediate, 0 device scalar) and uses it.
     Returns (gpu_outputs, oracle_outputs, ring_params) compared by the caller."""
     import torch
     from oracle import ring as R
@@ -155,6 +157,19 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
     os.environ.pop("MSCCL_CONFIG", None)
     dev = torch.device("cuda:0")
     comms = M.Comm.init_all([0] * nranks)
+    ops = [op] * nranks
+    dev_op, arg = op, 0
+    if op == N.AVG:
+        dev_op, arg = N.avg_op(dt, nranks)
+    scale_dev = None
+    if user_scale is not None:
+        value, residence = user_scale
+        dev_op, arg = N.PREMULSUM, N.scalar_bits(dt, value)
+        sb = int(arg).to_bytes(8, "little")[:N.type_size(dt)]
+        if residence == 0:
+            scale_dev = torch.frombuffer(bytearray(sb), dtype=torch.uint8).to(dev)
+            torch.cuda.synchronize()
+        ops = [c.create_premulsum(sb if residence == 1 else scale_dev.data_ptr(), dt, residence) for c in comms]
     try:
         if coll == L.ALLREDUCE:
             in_n, out_n = count, count
@@ -185,9 +200,9 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
             with M.group():
                 for r, c in enumerate(comms):
                     if coll == L.ALLREDUCE:
-                        c.all_reduce(sends[r], recvs[r], count, dt, op, stream)
+                        c.all_reduce(sends[r], recvs[r], count, dt, ops[r], stream)
                     elif coll == L.REDUCE_SCATTER:
-                        c.reduce_scatter(sends[r], recvs[r], count, dt, op, stream)
+                        c.reduce_scatter(sends[r], recvs[r], count, dt, ops[r], stream)
                     else:
                         c.all_gather(sends[r], recvs[r], count, dt, stream)
         torch.cuda.synchronize()
@@ -195,6 +210,9 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
             if c.async_error() != 0:
                 raise M.NcclError(c.async_error(), "kernel (async error)")
         gpu = [from_torch(t, N.storage(dt)) for t in t_out]
+        if user_scale is not None:
+            for c, o in zip(comms, ops):
+                c.destroy_op(o)
     finally:
         for c in comms:
             c.destroy()
@@ -207,7 +225,7 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
         o_out = [np.full(out_n, 7, N.storage(dt)) for _ in range(nranks)]
     res = None
     for _ in range(iters):
-        res, rp = R.run(coll, count, dt, op, o_in, o_out, in_place)
+        res, rp = R.run(coll, count, dt, dev_op, o_in, o_out, in_place, arg)
         if iters > 1 and coll == L.ALLREDUCE and in_place:
             o_in = res
     return gpu, [np.asarray(r) for r in res], rp

@@ -13,9 +13,9 @@ pytestmark = pytest.mark.gpu
 os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
 
 
-def check(n, coll, count, dt, op=0, in_place=True, seed=3, iters=1):
+def check(n, coll, count, dt, op=0, in_place=True, seed=3, iters=1, user_scale=None):
     from tests.gpu_harness import run_ring_fallback
-    gpu, ora, rp = run_ring_fallback(n, coll, count, dt, op, in_place, seed, iters=iters)
+    gpu, ora, rp = run_ring_fallback(n, coll, count, dt, op, in_place, seed, iters=iters, user_scale=user_scale)
     for r in range(n):
         g, o = gpu[r].view(np.uint8), ora[r].view(np.uint8)
         if not np.array_equal(g, o):
@@ -70,3 +70,90 @@ def test_ring_golden_vectors_on_gpu(name):
     gpu, _, _ = run_ring_fallback(n, coll, count, dt, op, inplace, seed=7)
     for r in range(n):
         assert np.array_equal(gpu[r].view(np.uint8), z["outputs"][r].view(np.uint8)), r
+
+
+# ---- ncclAvg and user PreMulSum ops (enqueue.cc:1388-1454, 1529-1580; reduce_kernel.h:498-687):
+# MSCCL never takes them (tuning.cc:345), the ring does: inputs scaled before the sum (floats) or
+# the sum divided after (integers).  LL sizes and Simple sizes, every element type.
+@pytest.mark.parametrize("dt", [7, 6, 9, 8, 2, 3, 0, 1, 4, 5])
+@pytest.mark.parametrize("count", [4099, 300001])
+def test_ring_avg_allreduce(dt, count):
+    check(3, L.ALLREDUCE, count, dt, op=4, in_place=True)
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("dt", [7, 9, 2])
+def test_ring_avg_allreduce_ranks_and_out_of_place(n, dt):
+    check(n, L.ALLREDUCE, 77777, dt, op=4, in_place=False)
+
+
+@pytest.mark.parametrize("dt", [7, 6, 2, 5])
+@pytest.mark.parametrize("in_place", [True, False])
+def test_ring_avg_reduce_scatter(dt, in_place):
+    check(4, L.REDUCE_SCATTER, 40001, dt, op=4, in_place=in_place)
+    check(4, L.REDUCE_SCATTER, 300007, dt, op=4, in_place=in_place)
+
+
+@pytest.mark.parametrize("dt,value", [(7, 0.37), (6, -1.75), (9, 3.0), (8, 0.1), (2, 3), (1, 7)])
+@pytest.mark.parametrize("residence", [1, 0])
+def test_ring_user_premulsum(dt, value, residence):
+    """ncclRedOpCreatePreMulSum with the scale in host memory (read at creation) or in device
+    memory (read by the kernel)."""
+    check(4, L.ALLREDUCE, 12345, dt, user_scale=(value, residence))
+    check(3, L.ALLREDUCE, 400001, dt, user_scale=(value, residence))
+
+
+def test_avg_one_rank_and_user_op_one_rank():
+    """nRanks == 1: ncclAvg is a copy (enqueue.cc:811-816), a user PreMulSum still scales the data
+    (oneRankReduce, onerank_reduce.cu:12-44), in place and out of place."""
+    import torch
+    import msccl_amd as M
+    from oracle import numerics as N
+    comm = M.Comm.init_all([0])[0]
+    try:
+        x = torch.randn(100003, device="cuda")
+        y = torch.zeros_like(x)
+        s = torch.cuda.current_stream().cuda_stream
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), x.numel(), M.FLOAT32, M.AVG, s)
+        torch.cuda.synchronize()
+        assert torch.equal(x, y)
+        op = comm.create_premulsum(np.float32(0.3).tobytes(), M.FLOAT32, M.SCALAR_HOST)
+        comm.all_reduce(x.data_ptr(), y.data_ptr(), x.numel(), M.FLOAT32, op, s)
+        z = x.clone()
+        comm.all_reduce(z.data_ptr(), z.data_ptr(), z.numel(), M.FLOAT32, op, s)
+        torch.cuda.synchronize()
+        want = N.pre_op(N.PREMULSUM, 7, x.cpu().numpy(), N.scalar_bits(7, 0.3))
+        assert np.array_equal(y.cpu().numpy().view(np.uint32), want.view(np.uint32))
+        assert np.array_equal(z.cpu().numpy().view(np.uint32), want.view(np.uint32))
+        comm.destroy_op(op)
+    finally:
+        comm.destroy()
+
+
+def test_user_op_errors():
+    """Builtin or unknown ops cannot be destroyed; a destroyed op, or one created on another
+    communicator or for another type, is rejected (enqueue.cc:1388-1454, 1563-1580)."""
+    import torch
+    import msccl_amd as M
+    comms = M.Comm.init_all([0, 0])
+    try:
+        x = torch.zeros(1024, device="cuda")
+        with pytest.raises(M.NcclError):
+            comms[0].destroy_op(M.SUM)
+        op0 = comms[0].create_premulsum(np.float32(2).tobytes(), M.FLOAT32)
+        op1 = comms[1].create_premulsum(np.float32(2).tobytes(), M.FLOAT32)
+        assert op0 >= 5 and op1 >= 5
+        if op0 != op1:   # mangled with the communicator: op0 means nothing to comms[1]
+            with pytest.raises(M.NcclError):
+                comms[1].all_reduce(x.data_ptr(), x.data_ptr(), 1024, M.FLOAT32, op0, 0)
+        with pytest.raises(M.NcclError):   # type mismatch
+            comms[0].all_reduce(x.data_ptr(), x.data_ptr(), 512, M.FLOAT16, op0, 0)
+        comms[0].destroy_op(op0)
+        with pytest.raises(M.NcclError):
+            comms[0].destroy_op(op0)
+        with pytest.raises(M.NcclError):
+            comms[0].all_reduce(x.data_ptr(), x.data_ptr(), 1024, M.FLOAT32, op0, 0)
+        comms[1].destroy_op(op1)
+    finally:
+        for c in comms:
+            c.destroy()

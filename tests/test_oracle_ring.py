@@ -73,9 +73,13 @@ def test_ring_plan_env(tmp_path, monkeypatch):
     assert prod["proto"] == rp["proto"] == L.PROTO_SIMPLE
     monkeypatch.setenv("MSCCL_AMD_RING_FALLBACK", "0")
     assert "ring" not in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 0, True)
-    # Avg has no ring in this build (PreMulSum/SumPostDiv are not provided)
+    # PreMulSum (ncclAvg on floats) is never MSCCL-eligible but runs on the ring; SumPostDiv only
+    # exists for integer types (reduce_kernel.h:498-520)
     monkeypatch.delenv("MSCCL_AMD_RING_FALLBACK")
-    assert "ring" not in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 4, True)
+    assert M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 4, True)["algo"] == -1
+    assert "ring" in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 4, True)
+    assert "ring" in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 2, 5, True)
+    assert "ring" not in M.plan_json(str(p), 0, 2, L.ALLREDUCE, 1000, 7, 5, True)
 
 
 from tests.golden import make_golden as G  # noqa: E402
@@ -89,3 +93,39 @@ def test_ring_golden(case):
     ins, outs = G.run_ring_case(n, coll, count, dt, op, inplace)
     assert np.array_equal(np.stack(ins), z["inputs"])
     assert np.array_equal(np.stack(outs).view(np.uint8), z["outputs"].view(np.uint8))
+
+
+def test_avg_lowering_matches_reference_host_code():
+    """hostToDevRedOp (enqueue.cc:1403-1431): integers -> SumPostDiv by n, floats -> PreMulSum by
+    1/n rounded through float (half: __float2half(float(1.0/n)))."""
+    from oracle import numerics as N
+    assert N.avg_op(2, 3) == (N.SUMPOSTDIV, 3)
+    assert N.avg_op(6, 3) == (N.PREMULSUM, 0x3555)          # 0.33325 in binary16
+    assert N.avg_op(9, 3) == (N.PREMULSUM, 0x3EAB)          # bf16 RNE of float(1/3) 0x3eaaaaab
+    assert N.avg_op(7, 8) == (N.PREMULSUM, 0x3E000000)      # 0.125f
+    assert N.avg_op(8, 4) == (N.PREMULSUM, 0x3FD0000000000000)
+
+
+def test_sumpostdiv_truncates_toward_zero():
+    from oracle import numerics as N
+    x = np.array([-7, 7, -1, 5, -128, 127], np.int8)
+    assert N.post_op(N.SUMPOSTDIV, 0, x, 2).tolist() == [-3, 3, 0, 2, -64, 63]
+    u = np.array([2 ** 64 - 1], np.uint64)
+    assert int(N.post_op(N.SUMPOSTDIV, 5, u, 3)[0]) == (2 ** 64 - 1) // 3
+
+
+@pytest.mark.parametrize("dt", [7, 6, 9, 2])
+def test_ring_avg_is_the_mean_for_power_of_two_ranks(dt):
+    """With 4 ranks and small-integer inputs every scaled value and partial sum is exact, so
+    the ring's Avg must be exactly the mean (integers: the truncated mean)."""
+    from oracle import numerics as N
+    from oracle import ring as R
+    from tests.gpu_harness import gen_inputs
+    n, count = 4, 3001
+    ins = gen_inputs(n, count, dt, 5, mode="exact")
+    dev_op, arg = N.avg_op(dt, n)
+    res, _ = R.run(L.ALLREDUCE, count, dt, dev_op, [x.copy() for x in ins], [None] * n, True, arg)
+    tot = np.sum([N.to_float64(dt, x) for x in ins], axis=0)
+    want = np.trunc(tot / n) if N.DTYPES[dt][2] == "int" else tot / n
+    for r in range(n):
+        assert np.array_equal(N.to_float64(dt, res[r]), want), r
