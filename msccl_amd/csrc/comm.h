@@ -23,6 +23,8 @@ constexpr uint64_t kCommMagic = 0x6d7363636c616d64ull;  // "msccl amd"
 // Connection key: (group, channel, peer); group = algorithm index, or kRingGroup for the ring
 // fallback's channels.  Every group owns its connections (transport.cc).
 constexpr int kRingGroup = kMaxAlgos;
+constexpr int kTreeGroup = kMaxAlgos + 1;  // the tree fallback's chain connections
+constexpr int kNumGroups = kMaxAlgos + 2;
 struct ConnKey {
   int group, chan, peer;
 };
@@ -57,7 +59,7 @@ struct ncclComm {
   std::vector<msccl::Algorithm> algos;
   std::vector<msccl::Registration> regs;
   std::vector<msccl::DevAlgoHost> devAlgos;
-  msccl::DevAlgoHost ringAlgos[4];  // ring fallback programs (transport.cc: ringUpload)
+  msccl::DevAlgoHost ringAlgos[5];  // ring fallback programs, [4] = tree (transport.cc: ringUpload)
   msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank
   bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank
   bool anyRemote = false;          // some peer runs on another GPU (xGMI): no LL128 unless allowed
@@ -71,11 +73,13 @@ struct ncclComm {
   std::vector<msccl::ConnKey> sendKeys, recvKeys;
   char* arena = nullptr;
   size_t arenaSize = 0;
-  std::vector<msccl::PeerOffsets> table;              // [(kMaxAlgos + 1) * kMaxChannels * nRanks] own table
+  std::vector<msccl::PeerOffsets> table;              // [kNumGroups * kMaxChannels * nRanks] own table
   std::vector<char*> peerArena;                        // per rank: mapped arena base
   std::vector<bool> peerArenaIpc;                      // opened through hipIpcOpenMemHandle
   msccl::DevSendConn* ringSend = nullptr;              // ring fallback connections [kRingChannels]
   msccl::DevRecvConn* ringRecv = nullptr;
+  msccl::DevSendConn* treeSend = nullptr;              // tree fallback connections [2 * kRingChannels]
+  msccl::DevRecvConn* treeRecv = nullptr;
   int llSlotLines = 0, simpleSlotBytes = 0;
   int buffSizes[3] = {0, 0, 0};
 

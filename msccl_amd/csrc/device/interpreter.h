@@ -816,7 +816,10 @@ struct Interp {
     const int64_t merge = w.merge;
     // ring fallback mode (w.ringColl != kRingNone): the reference's runRing loop over gridOffset
     const int ringColl = w.ringColl;
-    const int64_t ringSize = w.ringSize, nr = w.ringRanks, C = w.nBlocks;
+    // the tree runs two workgroups per channel: channel = bid / 2 (transport.cc: treePeers)
+    const bool tree = ringColl == kTreeAllReduce;
+    const int64_t ringSize = w.ringSize, nr = w.ringRanks, C = tree ? w.nBlocks / 2 : w.nBlocks;
+    const int64_t chan = tree ? bid >> 1 : bid;
     int64_t nelemGrid = 0;
     for (int64_t grid = 0, iter = 0; grid < (ringColl ? ringSize : sizePer) && !stop; grid += nelemGrid, iter++) {
       int64_t real;
@@ -824,7 +827,9 @@ struct Interp {
       if (ringColl) {
         const int64_t loop = ringColl == kRingAllReduce ? C * nr * chunkSize : C * chunkSize;
         const int64_t left = ringSize - grid;
-        if (ringColl == kRingAllReduce) {
+        if (tree) {
+          real = chunkSize;  // host-final chunk (runTreeUpDown / runTreeSplit: all_reduce.h:121-122)
+        } else if (ringColl == kRingAllReduce) {
           if constexpr (PROTO == pSimple) {  // all_reduce.h:43-46
             real = (left + C * nr - 1) / (C * nr);
             real = real < chunkSize ? real : chunkSize;
@@ -843,7 +848,7 @@ struct Interp {
           }
         }
         real = (int)real;
-        ringCo = grid + bid * real;
+        ringCo = grid + chan * real;
         nelemGrid = loop;
       } else if constexpr (PROTO == pSimple) {
         real = sizePer - grid < chunkSize ? sizePer - grid : chunkSize;

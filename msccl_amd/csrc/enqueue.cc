@@ -127,10 +127,12 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   return ncclSuccess;
 }
 
-// Ring fallback: one workgroup per ring channel, the reference's runRing program in ring mode.
+// Ring fallback: one workgroup per ring channel, the reference's runRing program in ring mode;
+// tree fallback: two workgroups per channel (reduce up, broadcast down).
 RankWork makeRingWork(Planned& p) {
   ncclComm* comm = p.op.comm;
-  const int kind = p.plan.ringColl == kRingAllReduce ? 0 : p.plan.ringColl == kRingReduceScatter ? 1
+  const int kind = p.plan.ringColl == kTreeAllReduce ? 4
+                   : p.plan.ringColl == kRingAllReduce ? 0 : p.plan.ringColl == kRingReduceScatter ? 1
                    : p.inPlace ? 2 : 3;
   const DevAlgoHost& da = comm->ringAlgos[kind];
   RankWork w;
@@ -158,7 +160,7 @@ RankWork makeRingWork(Planned& p) {
   w.minChunk = p.plan.minChunk;
   w.split = 1;
   w.merge = 1;
-  w.nBlocks = (int16_t)p.plan.ringChannels;
+  w.nBlocks = (int16_t)(p.plan.ringChannels * (kind == 4 ? 2 : 1));
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = 1;
   w.ringColl = (uint8_t)p.plan.ringColl;

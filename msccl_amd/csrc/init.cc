@@ -275,6 +275,8 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
     if (d.dImages) hipFree(d.dImages);  // their connection records are comm->ringSend / ringRecv
   if (comm->ringSend) hipFree(comm->ringSend);
   if (comm->ringRecv) hipFree(comm->ringRecv);
+  if (comm->treeSend) hipFree(comm->treeSend);
+  if (comm->treeRecv) hipFree(comm->treeRecv);
   for (size_t r = 0; r < comm->peerArena.size(); r++)
     if (comm->peerArenaIpc[r] && comm->peerArena[r]) hipIpcCloseMemHandle(comm->peerArena[r]);
   if (comm->dComm) hipFree(comm->dComm);

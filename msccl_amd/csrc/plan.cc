@@ -70,6 +70,9 @@ Knobs Knobs::fromEnv() {
   k.merge = (int32_t)envInt("MSCCL_AMD_MERGE", 0);
   k.ringFallback = envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0;
   k.ll128Remote = envInt("MSCCL_AMD_LL128_REMOTE", 0) != 0;
+  k.ringOn = listEnables(getenv("NCCL_ALGO"), "Ring", true);
+  k.treeOn = listEnables(getenv("NCCL_ALGO"), "Tree", true);
+  k.treeMaxBytes = envInt("MSCCL_AMD_TREE_MAX_BYTES", -1);  // -1: 16 KiB per rank (makeRingPlan)
   return k;
 }
 
@@ -198,11 +201,52 @@ int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverri
   return 0;
 }
 
+// The reference's tree AllReduce (all_reduce.h:103-298) on this build's chain (rank order, root
+// 0; the reference's intra-node trees are chains too): chunk math of computeColl for the tree
+// (enqueue.cc:634-644, Simple: the step halved while the loop is short relative to the tree
+// depth, n here) and of runTreeUpDown/runTreeSplit (loopSize > size: chunkSize =
+// divUp(size, nChannels * minChunkSize) * minChunkSize).
+static int makeTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
+  const int ts = refTypeSize(p->dtype);
+  const int64_t C = p->ringChannels;
+  int nt;
+  int64_t chunk, minChunk;
+  if (p->proto == kProtoLL) {
+    nt = clampNthreads(k.nthreads, 2 * kRefWarp, 512, 512);
+    chunk = k.buffSizes[kProtoLL] / kFifoSteps * 8 / 16 / ts;   // calcBytePerStep / sizeof(T)
+    minChunk = (int64_t)nt * 8 / ts;                             // nthreads * calcBytePerGrain / sizeof(T)
+  } else {
+    nt = clampNthreads(k.nthreads, 2 * kRefWarp, 512, 512) + kRefWarp + 3 * kRefWarp;  // enqueue.cc:516-520
+    int64_t cb = k.buffSizes[kProtoSimple] / kFifoSteps;         // stepSize, chunkSteps 1 for the tree
+    const int64_t depth = c.nRanks;
+    while (p->nBytes / (C * cb) < depth * 8 && cb > 131072) cb /= 2;
+    while (p->nBytes / (C * cb) < depth * 4 && cb > 65536) cb /= 2;
+    while (p->nBytes / (C * cb) < depth && cb > 32768) cb /= 2;
+    chunk = cb / ts;                                             // lastChunkSize
+    minChunk = (int64_t)(nt - 2 * kRefWarp) * 8 * (8 / ts);
+  }
+  if (C * chunk > p->count) chunk = (p->count + C * minChunk - 1) / (C * minChunk) * minChunk;
+  p->refNthreads = nt;
+  p->chunkSize = chunk;
+  p->minChunk = minChunk;
+  p->ringColl = kTreeAllReduce;
+  return 0;
+}
+
 int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   *p = Plan();
   p->algoIndex = -1;
   if (c.redop < 0 || c.redop > kDevSumPostDiv) return 5;
   if (c.redop == kDevSumPostDiv && !(c.dtype <= 5)) return 5;  // SumPostDiv is for integer types
+  // Small AllReduces take the tree: every chain thread block runs one transfer per chunk where a
+  // ring thread block runs 2(n-1), so the tree wins while latency dominates.  Measured on
+  // co-resident ranks, fp16 (profiles/r02_fallback_ring_tree.txt): 2 ranks 128 B 11.7 -> 8.0 us,
+  // 64 KiB ring ahead (16.3 vs 18.1); 8 ranks 128 B 35.9 -> 17.7 us, 64 KiB 52.6 -> 45.3 us,
+  // 1 MiB ring ahead (64 vs 85).  Default threshold: 16 KiB per rank.
+  const int64_t treeMax = k.treeMaxBytes >= 0 ? k.treeMaxBytes : (int64_t)16384 * c.nRanks;
+  const bool tree = c.coll == kAllReduce && k.treeOn &&
+                    (!k.ringOn || (int64_t)c.count * refTypeSize(c.dtype) <= treeMax);
+  if (!tree && !k.ringOn) return 5;
   if (c.coll == kAllReduce) p->ringColl = kRingAllReduce;
   else if (c.coll == kReduceScatter) p->ringColl = kRingReduceScatter;
   else if (c.coll == kAllGather) p->ringColl = kRingAllGather;
@@ -215,6 +259,7 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   const int64_t forced = k.ringChannels;
   int64_t ch = forced > 0 ? forced : std::max<int64_t>(1, p->nBytes >> 18);
   p->ringChannels = (int)std::max<int64_t>(1, std::min<int64_t>(kRingChannels, ch));
+  if (tree) return makeTreePlan(c, k, p);
   const int64_t* bs = k.buffSizes;
   int nt;
   if (p->proto == kProtoLL) {

@@ -41,7 +41,8 @@ struct Plan {
   int64_t minChunk = 0;     // LL: nthreads*8/ts; Simple: (nthreads-32)*8/ts
   size_t scratchNeeded = 0;
   int nIters = 0;
-  // ring fallback (algoIndex == -1): kRingAllReduce / kRingReduceScatter / kRingAllGather
+  // ring / tree fallback (algoIndex == -1): kRingAllReduce / kRingReduceScatter / kRingAllGather /
+  // kTreeAllReduce (chunkSize is then the final per-channel chunk of the tree loop)
   int ringColl = 0;
   int ringChannels = 0;
   int64_t ringLastChunk = 0;  // LL ReduceScatter / AllGather lastChunkSize (elements)
@@ -63,6 +64,8 @@ struct Knobs {
   int32_t merge;             // MSCCL_AMD_MERGE (0 = as many as fit)
   int32_t ringFallback;      // MSCCL_AMD_RING_FALLBACK
   int32_t ll128Remote;       // MSCCL_AMD_LL128_REMOTE: allow LL128 towards peers on other GPUs
+  int32_t ringOn, treeOn;    // NCCL_ALGO enables Ring / Tree for the fallback (tuning.cc:188-197)
+  int64_t treeMaxBytes;      // MSCCL_AMD_TREE_MAX_BYTES: AllReduce fallback calls up to this size take the tree
   static Knobs fromEnv();
 };
 

@@ -31,7 +31,7 @@ size_t alignUp(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 // Protocols whose FIFO memory a group needs (LL and LL128 share the LL FIFO).
 uint8_t groupProtoMask(const ncclComm* comm, int group) {
-  if (group == kRingGroup) return (uint8_t)((1u << kProtoLL) | (1u << kProtoSimple));
+  if (group == kRingGroup || group == kTreeGroup) return (uint8_t)((1u << kProtoLL) | (1u << kProtoSimple));
   uint8_t m = (uint8_t)(1u << comm->algos[group].proto);
   for (auto& r : comm->regs)
     if (r.algoIndex == group) m |= (uint8_t)(1u << r.proto);
@@ -40,8 +40,27 @@ uint8_t groupProtoMask(const ncclComm* comm, int group) {
 }
 
 int groupSubs(const ncclComm* comm, int group) {
-  if (group == kRingGroup) return 1;  // the ring runs unsplit
+  if (group == kRingGroup || group == kTreeGroup) return 1;  // the ring and the tree run unsplit
   return comm->algoSplit.empty() ? 1 : comm->algoSplit[group];
+}
+// The tree fallback's chain (rank order, root 0): thread block 2c+0 reduces up (receives from
+// the child, sends to the parent; the root sends its result back down to the child), 2c+1
+// broadcasts down (receives from the parent, sends to the child; empty on the root).
+void treePeers(int rank, int n, std::vector<int>* sp, std::vector<int>* rp) {
+  const int parent = rank - 1, child = rank + 1 < n ? rank + 1 : -1;
+  sp->assign(2 * kRingChannels, -1);
+  rp->assign(2 * kRingChannels, -1);
+  for (int c = 0; c < kRingChannels; c++) {
+    if (rank == 0) {
+      (*rp)[2 * c] = child;
+      (*sp)[2 * c] = child;
+    } else {
+      (*rp)[2 * c] = child;
+      (*sp)[2 * c] = parent;
+      (*rp)[2 * c + 1] = parent;
+      (*sp)[2 * c + 1] = child;
+    }
+  }
 }
 }  // namespace
 
@@ -98,16 +117,23 @@ ncclResult_t transportPlan(ncclComm* comm) {
       }
     }
   }
-  // ring fallback: ring channel c sends to rank+1 and receives from rank-1 (one sub-connection)
+  // ring fallback: ring channel c sends to rank+1 and receives from rank-1 (one sub-connection);
+  // tree fallback: the chain's up / down thread blocks of channel c
   if (comm->ringFallback && n > 1) {
     for (int c = 0; c < kRingChannels; c++) {
       comm->sendKeys.push_back(ConnKey{kRingGroup, c, (comm->rank + 1) % n});
       comm->recvKeys.push_back(ConnKey{kRingGroup, c, (comm->rank + n - 1) % n});
     }
+    std::vector<int> sp, rp;
+    treePeers(comm->rank, n, &sp, &rp);
+    for (int b = 0; b < 2 * kRingChannels; b++) {
+      if (sp[b] >= 0) comm->sendKeys.push_back(ConnKey{kTreeGroup, b / 2, sp[b]});
+      if (rp[b] >= 0) comm->recvKeys.push_back(ConnKey{kTreeGroup, b / 2, rp[b]});
+    }
   }
   const int64_t llBytes = (int64_t)alignUp((size_t)kLLFifoSlots * comm->llSlotLines * 16, kFifoAlign);
   const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
-  comm->table.assign((size_t)(kMaxAlgos + 1) * kMaxChannels * n,
+  comm->table.assign((size_t)kNumGroups * kMaxChannels * n,
                      PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
   size_t off = 0;
   for (auto& k : comm->sendKeys) {
@@ -229,6 +255,11 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
     for (int c = 0; c < kRingChannels; c++) ch[c] = c;
     NCCLCHECK(buildConns(comm, kRingGroup, kRingChannels, sp, rp, ch, tables, peerBases, peerRemote, &comm->ringSend,
                          &comm->ringRecv));
+    std::vector<int> tsp, trp, tch(2 * kRingChannels);
+    treePeers(comm->rank, n, &tsp, &trp);
+    for (int b = 0; b < 2 * kRingChannels; b++) tch[b] = b / 2;
+    NCCLCHECK(buildConns(comm, kTreeGroup, 2 * kRingChannels, tsp, trp, tch, tables, peerBases, peerRemote,
+                         &comm->treeSend, &comm->treeRecv));
   }
   return ncclSuccess;
 }
@@ -332,6 +363,45 @@ ncclResult_t ringUpload(ncclComm* comm) {
       h.hasSend = h.hasRecv = 1;
       h.nsteps = (uint16_t)prog.size();
       putImage(img, (size_t)c * d.tbStride, h, prog, none, none, none);
+    }
+    NCCLCHECK(uploadImages(img, &d));
+  }
+  {
+    // tree AllReduce (all_reduce.h:103-298, split form): offsets are -1 = the chunk offset
+    const int r = comm->rank;
+    std::vector<int> sp, rp;
+    treePeers(r, n, &sp, &rp);
+    auto one = [](uint8_t type, uint8_t sb, uint8_t db) {
+      Transfer t;
+      t.type = type;
+      t.srcbuf = sb;
+      t.srcoff = -1;
+      t.dstbuf = db;
+      t.dstoff = -1;
+      t.count = 1;
+      return std::vector<Transfer>{t};
+    };
+    std::vector<Transfer> up, down;
+    if (r == 0) up = one(kRecvReduceCopySend, kInput, kOutput);   // recv child, reduce, result down
+    else if (r == n - 1) up = one(kSend, kInput, kInput);         // leaf: send up
+    else up = one(kRecvReduceSend, kInput, kInput);               // recv child, reduce, send up
+    if (r == n - 1) down = one(kRecv, kInput, kOutput);           // leaf: receive the result
+    else if (r > 0) down = one(kRecvCopySend, kInput, kOutput);   // receive, keep, pass down
+    DevAlgoHost& d = comm->ringAlgos[4];
+    d.nBlocks = 2 * kRingChannels;
+    d.tbStride = (int)imageBytes(1, 0, 0);
+    d.connSplit = 1;
+    d.dSend = comm->treeSend;
+    d.dRecv = comm->treeRecv;
+    std::vector<char> img((size_t)d.tbStride * d.nBlocks, 0);
+    for (int b = 0; b < d.nBlocks; b++) {
+      const std::vector<Transfer>& prog = (b & 1) ? down : up;
+      DevTbHeader h;
+      memset(&h, 0, sizeof(h));
+      h.hasSend = sp[b] >= 0;
+      h.hasRecv = rp[b] >= 0;
+      h.nsteps = (uint16_t)prog.size();
+      putImage(img, (size_t)b * d.tbStride, h, prog, none, none, none);
     }
     NCCLCHECK(uploadImages(img, &d));
   }

@@ -21,7 +21,12 @@ msccl_amd/csrc/plan.cc (makeRingPlan) mirrors it:
   * the ring order is the rank order: ringRanks of rank r = [r, r+1, ..., r-1] (mod n);
   * channels = min(32, max(1, nBytes >> 18)) (MSCCL_AMD_RING_CHANNELS forces it);
   * LL when nBytes <= 512 KiB, else Simple (NCCL_PROTO masks them; LL128 is not used here);
-  * nThreads is not reduced for small messages (the reference halves it below its thresholds).
+  * nThreads is not reduced for small messages (the reference halves it below its thresholds);
+  * AllReduce calls of at most MSCCL_AMD_TREE_MAX_BYTES (default 16 KiB per rank), or all of them when
+    NCCL_ALGO enables Tree but not Ring, take the tree: the reference's runTreeSplit
+    (all_reduce.h:174-276) on a chain in rank order (root 0, parent r-1, child r+1), with
+    computeColl's tree chunk math (enqueue.cc:634-644; tree depth = nranks) and the kernel's
+    loopSize > size shrink (all_reduce.h:121-122).
 """
 from __future__ import annotations
 
@@ -47,6 +52,43 @@ def _proto_enabled(name: str) -> bool:
     names = [x.strip().lower() for x in (s[1:] if inv else s).split(",")]
     found = name.lower() in names
     return not found if inv else found
+
+
+def _algo_enabled(name: str) -> bool:
+    s = os.environ.get("NCCL_ALGO")
+    if s is None:
+        return True
+    inv = s.startswith("^")
+    names = [x.strip().lower() for x in (s[1:] if inv else s).split(",")]
+    found = name.lower() in names
+    return not found if inv else found
+
+
+def tree_params(rp: dict, nranks: int) -> dict:
+    """The tree variant of a fallback AllReduce (plan.cc: makeTreePlan)."""
+    ts, C, size, nbytes = rp["ts"], rp["channels"], rp["size"], rp["nbytes"]
+    bs = P.buff_sizes()
+    if rp["proto"] == L.PROTO_LL:
+        nthreads = P.max_threads(L.PROTO_LL)
+        chunk = bs[0] // P.NCCL_STEPS * 8 // 16 // ts
+        min_chunk = nthreads * 8 // ts
+    else:
+        nthreads = P.max_threads(L.PROTO_SIMPLE) + REF_WARP + 3 * REF_WARP
+        cb = bs[2] // P.NCCL_STEPS
+        depth = nranks
+        while nbytes // (C * cb) < depth * 8 and cb > 131072:
+            cb //= 2
+        while nbytes // (C * cb) < depth * 4 and cb > 65536:
+            cb //= 2
+        while nbytes // (C * cb) < depth and cb > 32768:
+            cb //= 2
+        chunk = cb // ts
+        min_chunk = (nthreads - 2 * REF_WARP) * 8 * (8 // ts)
+    if C * chunk > size:
+        chunk = -(-size // (C * min_chunk)) * min_chunk
+    out = dict(rp)
+    out.update({"algo": "tree", "nthreads": nthreads, "chunk": chunk, "min_chunk": min_chunk})
+    return out
 
 
 def ring_params(coll: int, count: int, dtype: int, nranks: int) -> Optional[dict]:
@@ -85,8 +127,43 @@ def ring_params(coll: int, count: int, dtype: int, nranks: int) -> Optional[dict
         align = nthreads * 8
         last = -(-last // align) * align
         last //= ts
-    return {"coll": coll, "size": size, "dtype": dt, "nbytes": nbytes, "proto": proto, "channels": chans,
-            "nthreads": nthreads, "chunk": chunk, "min_chunk": min_chunk, "last_chunk": last, "ts": ts}
+    rp = {"coll": coll, "size": size, "dtype": dt, "nbytes": nbytes, "proto": proto, "channels": chans,
+          "nthreads": nthreads, "chunk": chunk, "min_chunk": min_chunk, "last_chunk": last, "ts": ts,
+          "algo": "ring"}
+    tree_max = int(os.environ.get("MSCCL_AMD_TREE_MAX_BYTES", "-1") or -1)
+    if tree_max < 0:
+        tree_max = 16384 * nranks
+    ring_ok, tree_ok = _algo_enabled("Ring"), _algo_enabled("Tree")
+    if coll == L.ALLREDUCE and tree_ok and (not ring_ok or count * N.type_size(dtype) <= tree_max):
+        return tree_params(rp, nranks)
+    if not ring_ok:
+        return None
+    return rp
+
+
+def tree_ops(rp: dict, rank: int, n: int, bid: int):
+    """Channel bid // 2 of the chain tree: bid even reduces up, bid odd broadcasts down.  Yields
+    (kind, src_off, dst_off, nelem, recv_peer, send_peer)."""
+    size, C, chunk = rp["size"], rp["channels"], rp["chunk"]
+    c, up = bid // 2, bid % 2 == 0
+    parent, child = rank - 1, rank + 1 if rank + 1 < n else -1
+    grid = 0
+    while grid < size:
+        off = grid + c * chunk
+        ne = max(0, min(chunk, size - off))
+        if up:
+            if rank == 0:
+                yield ("rrcs", off, off, ne, child, child)          # recvReduceCopySend, postOp
+            elif child < 0:
+                yield ("s", off, None, ne, -1, parent)
+            else:
+                yield ("rrs", off, None, ne, child, parent)
+        elif rank > 0:
+            if child < 0:
+                yield ("r", None, off, ne, parent, -1)
+            else:
+                yield ("rcs", None, off, ne, parent, child)         # directRecvCopySend
+        grid += C * chunk
 
 
 def ops(rp: dict, rank: int, n: int, bid: int):
@@ -180,12 +257,19 @@ def run(coll: int, count: int, dtype: int, op: int, inputs: Sequence[np.ndarray]
         outs.append(out)
     fifos: Dict[Tuple[int, int, int], List[np.ndarray]] = {}
 
+    def steps(r, bid):
+        if rp["algo"] == "tree":
+            for kind, so, do, ne, src, dst in tree_ops(rp, r, n, bid):
+                yield kind, so, do, ne, (bid // 2, src, r), (bid // 2, r, dst)
+        else:
+            for kind, so, do, ne in ops(rp, r, n, bid):
+                yield kind, so, do, ne, (bid, (r - 1) % n, r), (bid, r, (r + 1) % n)
+
     def prog(r, bid):
-        nxt, prv = (r + 1) % n, (r - 1) % n
-        for kind, so, do, ne in ops(rp, r, n, bid):
+        for kind, so, do, ne, rkey, skey in steps(r, bid):
             msg = None
             if kind in ("rrs", "rrcs", "rcs", "r", "rrc"):
-                key = (bid, prv, r)
+                key = rkey
                 while not fifos.get(key):
                     yield False
                 msg = fifos[key].pop(0)
@@ -195,12 +279,12 @@ def run(coll: int, count: int, dtype: int, op: int, inputs: Sequence[np.ndarray]
                 v = outs[r][do:do + ne].copy() if in_place else ins[r][so:so + ne].copy()
                 if not in_place:
                     outs[r][do:do + ne] = v
-                fifos.setdefault((bid, r, nxt), []).append(v)
+                fifos.setdefault(skey, []).append(v)
             elif kind == "s":
                 v = ins[r][so:so + ne].copy()
                 if coll != L.ALLGATHER:
                     v = N.pre_op(op, dt, v, arg)
-                fifos.setdefault((bid, r, nxt), []).append(v)
+                fifos.setdefault(skey, []).append(v)
             elif kind in ("rrs", "rrcs", "rrc"):
                 local = N.pre_op(op, dt, ins[r][so:so + ne].copy(), arg)
                 if rp["proto"] == L.PROTO_SIMPLE:
@@ -212,15 +296,16 @@ def run(coll: int, count: int, dtype: int, op: int, inputs: Sequence[np.ndarray]
                 if kind in ("rrcs", "rrc"):
                     outs[r][do:do + ne] = v
                 if kind in ("rrs", "rrcs"):
-                    fifos.setdefault((bid, r, nxt), []).append(v)
+                    fifos.setdefault(skey, []).append(v)
             elif kind == "rcs":
                 outs[r][do:do + ne] = msg
-                fifos.setdefault((bid, r, nxt), []).append(msg)
+                fifos.setdefault(skey, []).append(msg)
             else:  # r
                 outs[r][do:do + ne] = msg
             yield True
 
-    live = [prog(r, b) for r in range(n) for b in range(rp["channels"])]
+    nb = rp["channels"] * (2 if rp["algo"] == "tree" else 1)
+    live = [prog(r, b) for r in range(n) for b in range(nb)]
     while live:
         progress, nxt_live = False, []
         for g in live:

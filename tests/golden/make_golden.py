@@ -87,7 +87,11 @@ def run_case(xml, n, coll, count, dt, op, inplace, mode, seed=7):
 
 
 def run_ring_case(n, coll, count, dt, op, inplace, seed=7):
+    """The RING_CASES fixtures are ring fallback outputs (small AllReduces would take the tree by
+    default, oracle/ring.py): the ring is pinned."""
     from oracle import ring as R
+    os.environ["NCCL_ALGO"] = "Ring,Tree"
+    os.environ["MSCCL_AMD_TREE_MAX_BYTES"] = "0"
     in_n = count * n if coll == L.REDUCE_SCATTER else count
     ins = gen_inputs(n, in_n, dt, seed, "uniform")
     if coll == L.ALLGATHER:

@@ -10,6 +10,14 @@ import pytest
 from oracle import loader as L
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _ring_algorithm(monkeypatch):
+    """These cases pin the ring (small AllReduces take the tree by default: plan.cc makeRingPlan);
+    the tree tests select it themselves."""
+    monkeypatch.setenv("NCCL_ALGO", "Ring,Tree")
+    monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", "0")
 os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
 
 
@@ -157,3 +165,32 @@ def test_user_op_errors():
     finally:
         for c in comms:
             c.destroy()
+
+
+# ---- tree fallback (all_reduce.h:103-298 on a chain, NCCL_ALGO=Tree) -----------------------------
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("count", [1, 37, 4099, 100003, 1234567])
+@pytest.mark.parametrize("dt", [7, 6, 9])
+def test_tree_allreduce(monkeypatch, n, count, dt):
+    monkeypatch.setenv("NCCL_ALGO", "Tree")
+    rp = check(n, L.ALLREDUCE, count, dt)
+    assert rp["algo"] == "tree"
+
+
+@pytest.mark.parametrize("op", [1, 2, 3, 4])
+@pytest.mark.parametrize("dt", [7, 2])
+def test_tree_ops_out_of_place_and_avg(monkeypatch, op, dt):
+    monkeypatch.setenv("NCCL_ALGO", "Tree")
+    check(4, L.ALLREDUCE, 77777, dt, op=op, in_place=False)
+    check(4, L.ALLREDUCE, 777777, dt, op=op, in_place=True)
+
+
+def test_tree_threshold_and_repeats(monkeypatch):
+    """MSCCL_AMD_TREE_MAX_BYTES routes small AllReduces to the tree and larger ones to the ring on
+    the same communicators; repeated launches keep both connection sets in step."""
+    monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", str(64 << 10))
+    assert check(4, L.ALLREDUCE, 5000, 7, iters=5)["algo"] == "tree"
+    monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES")        # default: 16 KiB per rank
+    assert check(4, L.ALLREDUCE, 16384, 7)["algo"] == "tree"
+    assert check(4, L.ALLREDUCE, 16385, 7)["algo"] == "ring"
+    assert check(4, L.ALLREDUCE, 50000, 7, iters=2)["algo"] == "ring"

@@ -141,7 +141,8 @@ def test_no_match_falls_back_to_ring(tmp_path):
             for b in o:
                 assert torch.equal(b.cpu(), x[0] + x[1]), (count, inplace)
         assert all(c.async_error() == 0 for c in comms)
-        assert comms[0].info()["sendConns"] == 4 + 32   # 4 all-pairs channels + 32 ring channels
+        # 4 all-pairs channels + 32 ring channels + 32 tree channels (rank 0 is the chain's root)
+        assert comms[0].info()["sendConns"] == 4 + 32 + 32
     finally:
         for c in comms:
             c.destroy()

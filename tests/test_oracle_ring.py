@@ -8,6 +8,14 @@ from msccl_amd import xmlgen
 from oracle import loader as L
 from oracle import ring as R
 
+@pytest.fixture(autouse=True)
+def _ring_algorithm(monkeypatch):
+    """These cases pin the ring (small AllReduces take the tree by default: plan.cc makeRingPlan);
+    the tree tests select it themselves."""
+    monkeypatch.setenv("NCCL_ALGO", "Ring,Tree")
+    monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", "0")
+
+
 
 @pytest.mark.parametrize("n", [2, 3, 5, 8])
 @pytest.mark.parametrize("count", [1, 7, 1000, 70001, 300001])
@@ -129,3 +137,41 @@ def test_ring_avg_is_the_mean_for_power_of_two_ranks(dt):
     want = np.trunc(tot / n) if N.DTYPES[dt][2] == "int" else tot / n
     for r in range(n):
         assert np.array_equal(N.to_float64(dt, res[r]), want), r
+
+
+@pytest.mark.parametrize("count,dt", [(1, 7), (999, 7), (40000, 6), (300001, 7), (5_000_000, 9)])
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_tree_plan_matches_product(tmp_path, monkeypatch, count, dt, n):
+    """NCCL_ALGO=Tree: the product's tree plan (plan.cc makeTreePlan) equals the oracle's restatement
+    of computeColl's tree chunk math and runTreeSplit's shrink."""
+    p = tmp_path / "none.xml"
+    p.write_text(xmlgen.allreduce_allpairs(2, 1, "LL", max_bytes=1))
+    monkeypatch.setenv("NCCL_ALGO", "Tree")
+    prod = M.plan_json(str(p), 0, n, L.ALLREDUCE, count, dt, 0, True)["ring"]
+    rp = R.ring_params(L.ALLREDUCE, count, dt, n)
+    assert rp["algo"] == "tree" and prod["coll"] == 4
+    assert (prod["proto"], prod["channels"], prod["chunk"], prod["minChunk"], prod["nthreads"]) == \
+        (rp["proto"], rp["channels"], rp["chunk"], rp["min_chunk"], rp["nthreads"])
+
+
+@pytest.mark.parametrize("dt", [7, 6, 2])
+@pytest.mark.parametrize("n", [2, 5])
+def test_tree_oracle_exact_and_chain_order(monkeypatch, dt, n):
+    """Exact-integer inputs give the exact sum on every rank; with LL the chain folds
+    fn(peer, local) upward: ((x[n-1] + x[n-2]) + ...) + x[0]."""
+    from tests.gpu_harness import gen_inputs
+    from oracle import numerics as N
+    monkeypatch.setenv("NCCL_ALGO", "Tree")
+    count = 70001
+    ins = gen_inputs(n, count, dt, 9, mode="exact")
+    res, rp = R.run(L.ALLREDUCE, count, dt, 0, [x.copy() for x in ins], [None] * n, True)
+    assert rp["algo"] == "tree"
+    tot = np.sum([N.to_float64(dt, x) for x in ins], axis=0)
+    for r in range(n):
+        assert np.array_equal(N.to_float64(dt, res[r]), tot)
+    ins = gen_inputs(n, 3001, 7, 4)
+    res, rp = R.run(L.ALLREDUCE, 3001, 7, 0, [x.copy() for x in ins], [None] * n, True)
+    acc = ins[n - 1]
+    for r in range(n - 2, -1, -1):
+        acc = N.apply(0, 7, acc, ins[r])
+    assert np.array_equal(res[0].view(np.uint32), acc.view(np.uint32))

@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=2)
     ap.add_argument("--instances", type=int, default=1)
     ap.add_argument("--proto", default="LL")
+    ap.add_argument("--dtype", type=int, default=7)
     ap.add_argument("--iters", type=int, default=300)
     a = ap.parse_args()
     import torch
@@ -23,17 +24,22 @@ def main():
            "pair": lambda: xmlgen.allreduce_pair_oneshot(a.instances, a.proto),
            "ring": lambda: xmlgen.allreduce_ring(a.ranks, a.instances, a.proto),
            "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2)}
-    path = "/tmp/lat_one_%d.xml" % os.getpid()
-    open(path, "w").write(gen[a.schedule]())
-    os.environ["MSCCL_XML_FILES"] = path
+    if a.schedule in ("fbring", "fbtree"):   # no schedule: the ring / tree fallback
+        os.environ.pop("MSCCL_XML_FILES", None)
+        os.environ["NCCL_ALGO"] = "Ring" if a.schedule == "fbring" else "Tree"
+    else:
+        path = "/tmp/lat_one_%d.xml" % os.getpid()
+        open(path, "w").write(gen[a.schedule]())
+        os.environ["MSCCL_XML_FILES"] = path
     comms = M.Comm.init_all([0] * a.ranks)
-    cnt = a.bytes // 4
-    bufs = [torch.ones(cnt, device="cuda") for _ in comms]
+    ts = {7: 4, 6: 2, 9: 2}[a.dtype]
+    cnt = a.bytes // ts
+    bufs = [torch.ones(cnt * ts // 4 + 1, device="cuda") for _ in comms]
 
     def step():
         with M.group():
             for c, b in zip(comms, bufs):
-                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, M.FLOAT32, M.SUM, 0)
+                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, 0)
     for _ in range(20):
         step()
     torch.cuda.synchronize()
