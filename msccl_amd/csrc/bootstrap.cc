@@ -8,6 +8,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -67,8 +68,14 @@ void rootLoop(int lfd, uint64_t nonce) {
     if (fd < 0) continue;
     int one = 1;
     setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+    // a connection that never sends its Hello (a stray client, a rank that died while
+    // connecting) must not stall the accept loop: bound the read, then drop the socket
+    struct timeval tv = {5, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
     Hello h;
     if (recvAll(fd, &h, sizeof(h)) || h.magic != kBootMagic || h.nonce != nonce) { close(fd); continue; }
+    struct timeval none = {0, 0};
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &none, sizeof(none));  // rounds may wait on slow ranks
     if (nRanks < 0) { nRanks = h.nRanks; byRank.assign(nRanks, -1); }
     if (h.nRanks != nRanks || h.rank < 0 || h.rank >= nRanks || byRank[h.rank] != -1) { close(fd); continue; }
     byRank[h.rank] = fd;
