@@ -108,7 +108,7 @@ struct ncclComm {
 
   // what the most recent collective ran (introspection: mscclAmdCommInfo "last")
   struct LastLaunch {
-    int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0;
+    int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0, small = 0;
   } last;
 
   // user reduction ops (ncclRedOpCreatePreMulSum, enqueue.cc:1529-1580): a free list as in the

@@ -196,6 +196,7 @@ typedef int (*OneRankFn)(const void* src, void* dst, size_t n, uint64_t arg, int
 OneRankFn getOneRankFn(int dtype);
 constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = resident workgroups per CU
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
+LaunchFn getSmallLaunchFn(int dtype, int redop);  // mscclSmallKernel (LL, Sum..Min), or null
 
 }  // namespace msccl
 

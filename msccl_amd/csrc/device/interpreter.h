@@ -743,31 +743,20 @@ struct Interp {
     }
   }
 
-  // ---------------------------------------------------------------- the interpreter loop
-  __device__ __forceinline__ void run(const RankWork& w, int bid, int sub) {
+  // ---------------------------------------------------------------- launch prologue / epilogue
+  // Prologue: one memory round trip.  The image (header + program), both connection records
+  // and the launch epoch sit at addresses known from the block index, so all of them are in
+  // flight together: image by every lane with a 16-B unit, records by lanes 0-3 / 64-67 (other
+  // waves), the epoch by a lane of a third wave.  Returns the launch epoch (workIndex).
+  __device__ __forceinline__ uint64_t prologue(const RankWork& w, int bid, int sub, DevTbHeader& hd) {
     tid = threadIdx.x;
     comm = w.comm;
     refNthreads = w.refNthreads;
-    t0 = __builtin_amdgcn_s_memrealtime();
     timeoutTicks = w.timeoutTicks;
-    redArg = w.redOpArg;
-    if (w.redOpArgIsPtr) {  // ncclScalarDevice: the scale lives in device memory (enqueue.cc:1549-1557)
-      T x;
-      __builtin_memcpy(&x, (const void*)w.redOpArg, sizeof(T));
-      redArg = 0;
-      __builtin_memcpy(&redArg, &x, sizeof(T));
-      redArg = uni(redArg);
-    }
     llFlagMask = w.llFlagMask;
     llCleanMask = w.llCleanMask;
-    const int split = w.split;
-    const int maxSplit = w.maxSplit;
-    const int slot = bid * maxSplit + sub;        // flag / epoch / trace slot of this workgroup
+    const int slot = bid * w.maxSplit + sub;      // flag / epoch / trace slot of this workgroup
     const int cslot = bid * w.connSplit + sub;    // its connection records
-    // Prologue: one memory round trip.  The image (header + program), both connection records
-    // and the launch epoch sit at addresses known from the block index, so all of them are in
-    // flight together: image by every lane with a 16-B unit, records by lanes 0-3 / 64-67 (other
-    // waves), the epoch by a lane of a third wave.
     {
       const u32x4* gimg = (const u32x4*)(w.images + (size_t)bid * w.tbStride);
       const int nU = w.tbStride >> 4;
@@ -780,7 +769,6 @@ struct Interp {
       }
     }
     __syncthreads();
-    DevTbHeader hd;
     {
       u32x4 raw = sh->img[0];
       raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
@@ -798,6 +786,99 @@ struct Interp {
     recvStep = rcG ? uni(sh->rconn.step) : 0;
     headSeen = scG ? uni(sh->sconn.headSeen) : 0;
     tailSeen = rcG ? uni(sh->rconn.tailSeen) : 0;
+    return uni(sh->epoch);  // COMPUTE_FLAG's workIndex (msccl_interpreter.h:14-16)
+  }
+
+  // Epilogue: persist the connection state and advance this slot's epoch, plus the epoch of
+  // every slot this launch does not run (DevComm::epochs): the subs [split, maxSplit) of each
+  // launched tb (by that tb's sub 0), and the slots of the tbs beyond the schedule's,
+  // [nTb * maxSplit, kFlagSlots), dealt over the launch's workgroups.
+  __device__ __forceinline__ void epilogue(const RankWork& w, int bid, int sub, uint64_t workIndex) {
+    const int split = w.split, maxSplit = w.maxSplit;
+    __syncthreads();
+    if (tid == 0) {
+      if (scG) {
+        scG->step = sendStep;
+        scG->headSeen = headSeen;
+      }
+      if (rcG) {
+        rcG->step = recvStep;
+        rcG->tailSeen = tailSeen;
+      }
+      atomicStoreAgent(w.epochs + bid * maxSplit + sub, workIndex + 1);
+    }
+    const int launched = w.nBlocks, nTb = launched / split, g = bid * split + sub;
+    if (sub == 0 && tid < maxSplit - split) atomicStoreAgent(w.epochs + bid * maxSplit + split + tid, workIndex + 1);
+    for (int j = nTb * maxSplit + g + tid * launched; j < kFlagSlots; j += kNT * launched)
+      atomicStoreAgent(w.epochs + j, workIndex + 1);
+  }
+
+  // Wait for the same positions of the thread blocks transfer t depends on
+  // (msccl_interpreter.h:123-140)
+  __device__ __forceinline__ void waitDeps(const DevTransfer& t, const uint64_t* flags, uint64_t workIndex,
+                                           uint64_t iter, int sub, int maxSplit) {
+    if (tid < t.numDeps) {
+      const int db = depBid[t.depPtr + tid];
+      const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)depStep[t.depPtr + tid]);
+      Spin spins;
+      while (true) {
+        uint64_t cur = atomicLoadAgent(flags + ((size_t)db * maxSplit + sub) * kFlagStride);
+        if (cur >= goal && (cur >> 24) == workIndex) break;
+        if (spinAbort(spins)) break;
+      }
+    }
+    __syncthreads();
+  }
+
+  // One primitive call of transfer t; false for MSCCL_RES_ADD / unknown types (the tb ends,
+  // msccl_interpreter.h:195-196).  `reOff` is the chunk offset of a fused reduction's sources.
+  __device__ __forceinline__ bool exec(const DevTransfer& t, T* srcP, T* dstP, int64_t srcoff, int64_t dstoff,
+                                       int64_t reOff, int64_t sizePer, const Shape& s) {
+    switch (t.type) {
+      case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
+      case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, s); break;
+      case tRCS: op<1, 1, 0, 1>(nullptr, dstP + dstoff, s); break;
+      case tRRS: op<1, 1, 1, 0>(srcP + srcoff, nullptr, s); break;
+      case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
+      case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
+      case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
+      case tCopySend: op<0, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
+      case tRe: reduce(srcP, red + t.redPtr, reOff, sizePer, t.numReds, dstP + dstoff, s); __syncthreads(); break;
+      default: return false;
+    }
+    return true;
+  }
+
+  static __device__ __forceinline__ DevTransfer loadTransfer(const DevTransfer* p) {
+    DevTransfer t;
+    u32x4 raw = *(const u32x4*)p;
+    raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
+    __builtin_memcpy(&t, &raw, sizeof(t));
+    return t;
+  }
+
+  __device__ __forceinline__ void publishFlag(uint64_t* flags, int slot, uint64_t workIndex, uint64_t iter, int step) {
+    drainStores();
+    __syncthreads();
+    if (tid == 0) atomicStoreAgent(flags + (size_t)slot * kFlagStride, computeFlag(workIndex, iter, step));
+  }
+
+  // ---------------------------------------------------------------- the interpreter loop
+  __device__ __forceinline__ void run(const RankWork& w, int bid, int sub) {
+    t0 = __builtin_amdgcn_s_memrealtime();
+    redArg = w.redOpArg;
+    if (w.redOpArgIsPtr) {  // ncclScalarDevice: the scale lives in device memory (enqueue.cc:1549-1557)
+      T x;
+      __builtin_memcpy(&x, (const void*)w.redOpArg, sizeof(T));
+      redArg = 0;
+      __builtin_memcpy(&redArg, &x, sizeof(T));
+      redArg = uni(redArg);
+    }
+    const int split = w.split;
+    const int maxSplit = w.maxSplit;
+    const int slot = bid * maxSplit + sub;
+    DevTbHeader hd;
+    const uint64_t workIndex = prologue(w, bid, sub, hd);
     trace = w.trace ? w.trace + (size_t)slot * w.traceEvents : nullptr;
     nev = 1;
     maxEv = w.traceEvents;
@@ -809,7 +890,6 @@ struct Interp {
     const int64_t sizePer = w.sizePerChunk;
     const int64_t chunkSize = w.chunkSize;
     const int mac = w.maxAllowedCount;
-    const uint64_t workIndex = uni(sh->epoch);  // COMPUTE_FLAG's workIndex (msccl_interpreter.h:14-16)
     uint64_t* flags = w.flags;
     bool stop = false;
 
@@ -874,26 +954,10 @@ struct Interp {
       const int q0 = (int)divNonNeg((int64_t)Qc * sub, split), q1 = (int)divNonNeg((int64_t)Qc * (sub + 1), split);
       int step = 0;
       for (int i = 0; i < hd.nsteps; i++) {
-        DevTransfer t;
-        {
-          u32x4 raw = *(const u32x4*)&tr[i];
-          raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
-          __builtin_memcpy(&t, &raw, sizeof(t));
-        }
+        const DevTransfer t = loadTransfer(&tr[i]);
         if (t.numDeps > 0) {
-          // the same positions of the thread blocks this transfer depends on (interpreter.h:123-140)
-          if (tid < t.numDeps) {
-            const int db = depBid[t.depPtr + tid];
-            const uint64_t goal = computeFlag(workIndex, iter, (uint64_t)depStep[t.depPtr + tid]);
-            Spin spins;
-            while (true) {
-              uint64_t cur = atomicLoadAgent(flags + ((size_t)db * maxSplit + sub) * kFlagStride);
-              if (cur >= goal && (cur >> 24) == workIndex) break;
-              if (spinAbort(spins)) break;
-            }
-          }
+          waitDeps(t, flags, workIndex, iter, sub, maxSplit);
           step += t.numDeps - 1;
-          __syncthreads();
           ev(kEvDepWait, (uint16_t)i, 0);
         }
         T* srcP = t.srcbuf == 0 ? thisInput : (t.srcbuf == 1 ? thisOutput : thisScratch);
@@ -907,6 +971,7 @@ struct Interp {
         // splitting a transfer its receiver moves whole would misalign the steps whenever a call
         // is not a whole number of slots).  Calls stay within kMaxRunSlots slots per
         // sub-connection, and so far below the 2 GiB reach of a buffer descriptor.
+        // (runSmall applies the same rule: the two ends may run different kernels.)
         int macT = (t.type != tRe && !ringColl && nelem == sizePer &&
                     (int64_t)nelem * t.count <= w.maxOpElems) ? t.count : mac;
         if ((int64_t)nelem * TS * macT > (int64_t)0x7fffff00) {
@@ -950,57 +1015,19 @@ struct Interp {
             s.npk = thisCount * s.Lq;
           }
           ev(kEvPrimBegin, (uint16_t)i, ((uint32_t)t.type << 24) | (uint32_t)min(s.npk * PE, 0xFFFFFF));
-          switch (t.type) {
-            case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
-            case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, s); break;
-            case tRCS: op<1, 1, 0, 1>(nullptr, dstP + dstoff, s); break;
-            case tRRS: op<1, 1, 1, 0>(srcP + srcoff, nullptr, s); break;
-            case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
-            case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
-            case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
-            case tCopySend: op<0, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
-            case tRe: {
-              reduce(srcP, red + t.redPtr, grid + (int64_t)c * sizePer, sizePer, t.numReds, dstP + dstoff, s);
-              if (c == 0) step += t.numReds - 1;
-              __syncthreads();
-              break;
-            }
-            default: stop = true; break;  // MSCCL_RES_ADD / unknown: the tb ends (interpreter.h:195-196)
+          if (!exec(t, srcP, dstP, srcoff, dstoff, grid + (int64_t)c * sizePer, sizePer, s)) {
+            stop = true;
+            break;
           }
-          if (stop) break;
+          if (t.type == tRe && c == 0) step += t.numReds - 1;
           ev(kEvPrimEnd, (uint16_t)i, 0);
         }
         if (stop) break;
-        if (t.hasDep) {
-          drainStores();
-          __syncthreads();
-          if (tid == 0)
-            atomicStoreAgent(flags + (size_t)slot * kFlagStride, computeFlag(workIndex, iter, step));
-        }
+        if (t.hasDep) publishFlag(flags, slot, workIndex, iter, step);
         step++;
       }
     }
-    __syncthreads();
-    if (tid == 0) {
-      if (scG) {
-        scG->step = sendStep;
-        scG->headSeen = headSeen;
-      }
-      if (rcG) {
-        rcG->step = recvStep;
-        rcG->tailSeen = tailSeen;
-      }
-      atomicStoreAgent(w.epochs + slot, workIndex + 1);
-    }
-    {
-      // advance the epoch of every slot this launch does not run (DevComm::epochs): the subs
-      // [split, maxSplit) of each launched tb (by that tb's sub 0), and the slots of the tbs
-      // beyond the schedule's, [nTb * maxSplit, kFlagSlots), dealt over the launch's workgroups
-      const int launched = w.nBlocks, nTb = launched / split, g = bid * split + sub;
-      if (sub == 0 && tid < maxSplit - split) atomicStoreAgent(w.epochs + bid * maxSplit + split + tid, workIndex + 1);
-      for (int j = nTb * maxSplit + g + tid * launched; j < kFlagSlots; j += kNT * launched)
-        atomicStoreAgent(w.epochs + j, workIndex + 1);
-    }
+    epilogue(w, bid, sub, workIndex);
     ev(kEvEnd, 0, 0);
     if (trace != nullptr && tid == 0) {
       TraceEvent h;
@@ -1010,6 +1037,69 @@ struct Interp {
       h.arg = (uint32_t)workIndex;
       trace[0] = h;
     }
+  }
+
+  // ---------------------------------------------------------------- small calls
+  // A launch whose every rank's call is one interpreter iteration (sizePerChunk <= chunkSize),
+  // outside the ring / tree fallback and without tracing (enqueue.cc: smallEligible).  Then
+  // grid = 0, nelem = sizePerChunk and the iteration needs no chunk arithmetic; every offset
+  // fits 32 bits and split is a power of two, so a workgroup's positions are shifts.  The
+  // transfers, their cut into calls (the same macT rule as run(), so each end of a connection
+  // may run either kernel) and the primitives are run()'s; what goes is the 64-bit iteration
+  // arithmetic and most of the scalar state the big loop keeps live (SGPR spills), which for a
+  // call of a few KiB is most of a launch.
+  __device__ __forceinline__ void runSmall(const RankWork& w, int local) {
+    redArg = 0;
+    trace = nullptr;
+    const int split = w.split;
+    const int lg = __builtin_ctz((unsigned)split);
+    const int bid = local >> lg, sub = local & (split - 1);
+    DevTbHeader hd;
+    const uint64_t workIndex = prologue(w, bid, sub, hd);
+    const int maxSplit = w.maxSplit;
+    T* const bufs[3] = {(T*)w.sendbuff, (T*)w.recvbuff, (T*)w.scratch};
+    const int nelem = (int)w.sizePerChunk;
+    const int mac = w.maxAllowedCount;
+    const int64_t maxOp = w.maxOpElems;
+    const uint32_t Qc = ((uint32_t)nelem + PE - 1) / PE;
+    const int q0 = (int)((Qc * (uint32_t)sub) >> lg), q1 = (int)((Qc * (uint32_t)(sub + 1)) >> lg);
+    int step = 0;
+    for (int i = 0; i < hd.nsteps; i++) {
+      const DevTransfer t = loadTransfer(&tr[i]);
+      if (t.numDeps > 0) {
+        waitDeps(t, w.flags, workIndex, 0, sub, maxSplit);
+        step += t.numDeps - 1;
+      }
+      T* srcP = bufs[t.srcbuf < 2 ? t.srcbuf : 2];
+      T* dstP = bufs[t.dstbuf < 2 ? t.dstbuf : 2];
+      const int macT = (t.type != tRe && (int64_t)nelem * t.count <= maxOp) ? t.count : mac;
+      bool stop = false;
+      for (int c = 0; c < t.count; c += macT) {
+        const int thisCount = macT < t.count - c ? macT : t.count - c;
+        Shape s;
+        s.n = nelem * thisCount;
+        if (split == 1) {
+          s.Q = (s.n + PE - 1) / PE;
+          s.q0 = 0;
+          s.Lq = s.Q;
+          s.npk = s.Q;
+        } else {
+          s.Q = (int)Qc;
+          s.q0 = q0;
+          s.Lq = q1 - q0;
+          s.npk = thisCount * s.Lq;
+        }
+        if (!exec(t, srcP, dstP, (t.srcoff + c) * nelem, (t.dstoff + c) * nelem, c * nelem, nelem, s)) {
+          stop = true;
+          break;
+        }
+        if (t.type == tRe && c == 0) step += t.numReds - 1;
+      }
+      if (stop) break;
+      if (t.hasDep) publishFlag(w.flags, bid * maxSplit + sub, workIndex, 0, step);
+      step++;
+    }
+    epilogue(w, bid, sub, workIndex);
   }
 };
 
@@ -1024,6 +1114,20 @@ __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
   it.run(w, local / w.split, local % w.split);
+}
+
+// Small-call variant (Interp::runSmall): every RankWork of the launch is one interpreter
+// iteration of an MSCCL schedule.
+template <typename T, int OP, int PROTO>
+__global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgs args) {
+  __shared__ BlockShared sh;
+  int b = blockIdx.x;
+  int r = 0;
+  while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
+  const RankWork& w = args.w[r];
+  Interp<T, OP, PROTO> it;
+  it.sh = &sh;
+  it.runSmall(w, b - w.blockBase);
 }
 
 }  // namespace msccl

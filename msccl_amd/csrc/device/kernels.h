@@ -19,6 +19,18 @@ int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// the small-call kernel (mscclSmallKernel, LL): same contract as launchKernel
+template <typename T, int OP, int PROTO>
+int launchSmallKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  if (gridBlocks == kQueryResidency) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclSmallKernel<T, OP, PROTO>, kNT, 0) != hipSuccess) return 0;
+    return n;
+  }
+  hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, args);
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // nRanks == 1 with a user PreMulSum op: dst = src * scale (the reference's oneRankReduce,
 // onerank_reduce.cu:12-44: ReduceOrCopyMulti with the preOp applied, postOp identity).
 template <typename T>
@@ -49,12 +61,18 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
       {launchKernel<T, kMax, pLL>, launchKernel<T, kMax, pLL128>, launchKernel<T, kMax, pSimple>},         \
       {launchKernel<T, kMin, pLL>, launchKernel<T, kMin, pLL128>, launchKernel<T, kMin, pSimple>},         \
       {launchKernel<T, kPreMulSum, pLL>, nullptr, launchKernel<T, kPreMulSum, pSimple>}
+// Small-call kernels: MSCCL schedules (ops Sum..Min) on LL.
+#define MSCCL_SMALL(NAME, T)                                                                               \
+  LaunchFn NAME##_small[4] = {launchSmallKernel<T, kSum, pLL>, launchSmallKernel<T, kProd, pLL>,          \
+                              launchSmallKernel<T, kMax, pLL>, launchSmallKernel<T, kMin, pLL>};
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \
                          {launchKernel<T, kSumPostDiv, pLL>, nullptr, launchKernel<T, kSumPostDiv, pSimple>}}; \
+  MSCCL_SMALL(NAME, T)                                                                                     \
   OneRankFn NAME##_one = launchOneRankScale<T>;
 #define MSCCL_DEFINE_TABLE_FP(NAME, T)                                                                     \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T), {nullptr, nullptr, nullptr}};                                   \
+  MSCCL_SMALL(NAME, T)                                                                                     \
   OneRankFn NAME##_one = launchOneRankScale<T>;
 
 }  // namespace msccl

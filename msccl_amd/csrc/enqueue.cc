@@ -246,6 +246,17 @@ RankWork makeWork(Planned& p) {
   return w;
 }
 
+// mscclSmallKernel takes a call that is one LL interpreter iteration of an MSCCL schedule, run
+// untraced, with a Sum..Min op (interpreter.h: runSmall).  Both kernels cut a
+// transfer into the same primitive calls, so ranks that choose differently still agree.
+bool smallEligible(const Planned& p, const RankWork& w) {
+  const ncclComm* comm = p.op.comm;
+  return comm->knobs.smallKernel && p.plan.ringColl == 0 && p.plan.proto == kProtoLL && p.op.devOp <= 3 &&
+         p.plan.nIters == 1 && p.plan.sizePerChunk <= p.plan.chunkSize && w.trace == nullptr &&
+         (w.split & (w.split - 1)) == 0 &&
+         p.plan.sizePerChunk * p.plan.nchunksPerLoop * refTypeSize(p.plan.dtype) <= (1ll << 30);
+}
+
 ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   ncclComm* c0 = ps[0]->op.comm;
   int dev = c0->cudaDev;
@@ -253,11 +264,13 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   LaunchArgs args;
   memset(&args, 0, sizeof(args));
   int blocks = 0;
+  bool small = true;
   for (size_t i = 0; i < ps.size(); i++) {
     RankWork w = makeWork(*ps[i]);
     w.blockBase = (int16_t)blocks;
     blocks += w.nBlocks;
     args.w[i] = w;
+    small = small && smallEligible(*ps[i], w);
   }
   args.nRanks = (int)ps.size();
   if (blocks == 0) return ncclSuccess;
@@ -271,7 +284,8 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
     }
   }
   const Planned& p0 = *ps[0];
-  LaunchFn fn = getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
+  LaunchFn fn = small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp) : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
+  for (Planned* p : ps) p->op.comm->last.small = small ? 1 : 0;
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {
     // Every workgroup of the launch may spin on every other one (FIFO credits, dependency

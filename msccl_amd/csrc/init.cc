@@ -115,12 +115,15 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
   }
   s.knobs = comm->knobs;
+  s.knobs.smallKernel = 0;  // a rank-local choice: both kernels cut the same FIFO steps
   return s;
 }
 
 ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
+  Knobs agreed = comm->knobs;
+  agreed.smallKernel = 0;
   for (size_t r = 0; r < recs.size(); r++) {
-    if (memcmp(&recs[r].knobs, &comm->knobs, sizeof(Knobs)) != 0) {
+    if (memcmp(&recs[r].knobs, &agreed, sizeof(Knobs)) != 0) {
       WARN("MSCCL: rank %zu runs with different NCCL_*/MSCCL_AMD_* settings than rank %d (NCCL_ALGO, NCCL_PROTO, "
            "NCCL_NTHREADS, NCCL_*BUFFSIZE, MSCCL_AMD_SPLIT/MERGE/TARGET_WGS/RING_CHANNELS/RING_FALLBACK/LL128_REMOTE "
            "must agree)", r, comm->rank);

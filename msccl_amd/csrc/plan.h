@@ -66,6 +66,7 @@ struct Knobs {
   int32_t ll128Remote;       // MSCCL_AMD_LL128_REMOTE: allow LL128 towards peers on other GPUs
   int32_t ringOn, treeOn;    // NCCL_ALGO enables Ring / Tree for the fallback (tuning.cc:188-197)
   int64_t treeMaxBytes;      // MSCCL_AMD_TREE_MAX_BYTES: AllReduce fallback calls up to this size take the tree
+  int32_t smallKernel;       // MSCCL_AMD_SMALL_KERNEL: one-iteration LL launches take mscclSmallKernel
   static Knobs fromEnv();
 };
 

@@ -1,0 +1,134 @@
+"""The small-call kernel (interpreter.h: runSmall, enqueue.cc: smallEligible).
+
+A launch whose calls are one LL interpreter iteration of an MSCCL schedule runs
+mscclSmallKernel.  It must give the reference's bits (oracle) exactly like the general kernel,
+the two must agree bit for bit, and two ranks that run different kernels must still
+interoperate (they cut every transfer into the same FIFO steps)."""
+import os
+
+import numpy as np
+import pytest
+
+import msccl_amd as M
+from msccl_amd import xmlgen
+from oracle import loader as L
+from tests.gpu_harness import CoResident, describe_mismatch, gen_inputs, to_torch, from_torch
+from oracle import numerics as N
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
+
+SCHEDULES = {
+    "pair2": (2, lambda: xmlgen.allreduce_pair_oneshot(1, "LL")),
+    "allpairs8": (8, lambda: xmlgen.allreduce_allpairs(8, 1, "LL")),   # C3's form: reductions + deps
+    "ring4": (4, lambda: xmlgen.allreduce_ring(4, 1, "LL")),
+}
+
+
+def _run(cr, count, dt, op, seed):
+    import torch
+    dev = torch.device("cuda:0")
+    ins = gen_inputs(cr.n, count, dt, seed)
+    t = [to_torch(x, dev) for x in ins]
+    torch.cuda.synchronize()
+    p = [x.data_ptr() for x in t]
+    cr.run(L.ALLREDUCE, count, dt, op, p, p)
+    return ins, [from_torch(x, N.storage(dt)) for x in t], [c.info()["last"] for c in cr.comms]
+
+
+@pytest.mark.parametrize("name", sorted(SCHEDULES))
+@pytest.mark.parametrize("count,dt,op", [(64, 7, 0), (320, 7, 2), (192, 7, 0), (1024, 6, 0), (16384, 9, 0),
+                                         (8192, 7, 3)])
+def test_small_kernel_matches_oracle_and_general(name, count, dt, op, tmp_path, monkeypatch):
+    n, gen = SCHEDULES[name]
+    xml = gen()
+    xp = tmp_path / "s.xml"
+    xp.write_text(xml)
+    one_iter = M.plan_json(str(xp), 0, n, L.ALLREDUCE, count, dt, op, True)["nIters"] == 1
+    outs = {}
+    for small in ("1", "0"):
+        monkeypatch.setenv("MSCCL_AMD_SMALL_KERNEL", small)
+        with CoResident(n, [xml], str(tmp_path)) as cr:
+            ins, got, last = _run(cr, count, dt, op, seed=11)
+            assert all(l["small"] == int(small == "1" and one_iter) for l in last), last
+            want, idx = cr.oracle(L.ALLREDUCE, count, dt, op, ins, True)
+            assert idx == 0
+            for r in range(n):
+                assert np.array_equal(got[r].view(np.uint8), want[r].view(np.uint8)), \
+                    "small=%s rank %d: %s" % (small, r, describe_mismatch(got[r], want[r]))
+            outs[small] = got
+    for r in range(n):
+        assert np.array_equal(outs["1"][r].view(np.uint8), outs["0"][r].view(np.uint8))
+
+
+def test_large_call_takes_general_kernel(tmp_path, monkeypatch):
+    """Several interpreter iterations: the general kernel runs (and still matches the oracle)."""
+    monkeypatch.setenv("MSCCL_AMD_SMALL_KERNEL", "1")
+    xml = xmlgen.allreduce_pair_oneshot(1, "LL")
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        count = 1 << 20
+        ins, got, last = _run(cr, count, 7, 0, seed=3)
+        assert all(l["small"] == 0 for l in last), last
+        want, _ = cr.oracle(L.ALLREDUCE, count, 7, 0, ins, True)
+        for r in range(2):
+            assert np.array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+
+
+def _mixed_proc(rank, world, xml_path, count, small, q_in, q_out):
+    import torch
+    os.environ["MSCCL_XML_FILES"] = xml_path
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "30"
+    os.environ["MSCCL_AMD_SMALL_KERNEL"] = small
+    torch.cuda.set_device(0)
+    uid = M.get_unique_id() if rank == 0 else None
+    if rank == 0:
+        for _ in range(world - 1):
+            q_in.put(uid)
+    else:
+        uid = q_in.get(timeout=60)
+    x = gen_inputs(world, count, 7, 9)[rank]
+    comm = M.Comm.init_rank(world, uid, rank)
+    t = to_torch(x, torch.device("cuda:0"))
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(5):
+        comm.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, s)
+    torch.cuda.synchronize()
+    err = comm.async_error()
+    last = comm.info()["last"]
+    out = t.cpu().numpy()
+    comm.destroy()
+    q_out.put((rank, err, last["small"], out))
+
+
+def test_mixed_kernels_across_processes(tmp_path):
+    """Rank 0 runs the small kernel, rank 1 the general one (MSCCL_AMD_SMALL_KERNEL is a
+    rank-local choice): the FIFO steps still line up and the values are the reference's."""
+    import torch.multiprocessing as mp
+    from oracle import plan as P, sim as S
+    world, count = 2, 3000  # 375 elements per chunk: not whole 16-B packs
+    xml = xmlgen.allreduce_allpairs(world, 2, "LL")
+    p = tmp_path / "ap.xml"
+    p.write_text(xml)
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_mixed_proc, args=(r, world, str(p), count, "1" if r == 0 else "0", q_in, q_out))
+          for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, small, out = q_out.get(timeout=300)
+        res[r] = (err, small, out)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert res[0][1] == 1 and res[1][1] == 0
+    algos = [L.parse_xml(xml, r, world) for r in range(world)]
+    call = P.Call(L.ALLREDUCE, count, 7, 0, world, 0, True)
+    plan = P.make_plan([algos[0]], call, 0)
+    ins = gen_inputs(world, count, 7, 9)
+    for _ in range(5):
+        ins, _st = S.run(algos, plan, ins, [None] * world, L.ALLREDUCE, True)
+    for r in range(world):
+        assert res[r][0] == 0
+        assert np.array_equal(res[r][2].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
