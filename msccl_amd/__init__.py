@@ -8,7 +8,6 @@ missing every entry point raises.
 """
 from __future__ import annotations
 
-import contextlib
 import ctypes
 import json
 import os
@@ -265,14 +264,18 @@ class Comm:
                "ncclCustomCollective")
 
 
-@contextlib.contextmanager
-def group():
-    """ncclGroupStart / ncclGroupEnd (nccl.h.in:369-380)."""
-    _check(lib().ncclGroupStart(), "ncclGroupStart")
-    try:
-        yield
-    finally:
+class group:
+    """ncclGroupStart / ncclGroupEnd (nccl.h.in:369-380) as a context manager (a class, not a
+    generator: it sits on the per-call path of small collectives)."""
+    __slots__ = ()
+
+    def __enter__(self):
+        _check(lib().ncclGroupStart(), "ncclGroupStart")
+        return self
+
+    def __exit__(self, *exc):
         _check(lib().ncclGroupEnd(), "ncclGroupEnd")
+        return False
 
 
 def torch_dtype_code(t) -> int:

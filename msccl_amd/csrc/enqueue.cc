@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <map>
 #include <thread>
+#include <tuple>
 #include <vector>
 
 #include "comm.h"
@@ -326,35 +327,49 @@ void groupAddInit(std::function<ncclResult_t()> fn, ncclComm* comm) { tInits.emp
 void groupAddOp(const CollOp& op) { tOps.push_back(op); }
 
 ncclResult_t executeOps(std::vector<CollOp>& ops) {
-  // rounds: the k-th op of every communicator runs in round k
+  // rounds: the k-th op of every communicator runs in round k.  The usual group holds one op per
+  // communicator (one round); nothing here allocates per call beyond the per-round vectors.
   std::vector<ncclComm*> order;
-  std::map<ncclComm*, std::vector<size_t>> perComm;
+  std::vector<std::vector<size_t>> perComm;  // parallel to `order`
+  order.reserve(ops.size());
   for (size_t i = 0; i < ops.size(); i++) {
-    if (!perComm.count(ops[i].comm)) order.push_back(ops[i].comm);
-    perComm[ops[i].comm].push_back(i);
+    size_t j = 0;
+    while (j < order.size() && order[j] != ops[i].comm) j++;
+    if (j == order.size()) {
+      order.push_back(ops[i].comm);
+      perComm.emplace_back();
+    }
+    perComm[j].push_back(i);
   }
   size_t rounds = 0;
-  for (auto& kv : perComm) rounds = std::max(rounds, kv.second.size());
+  for (auto& v : perComm) rounds = std::max(rounds, v.size());
   int saved = 0;
   hipGetDevice(&saved);
+  int cur = saved;
+  auto setDev = [&cur](int d) {
+    if (d != cur) {
+      hipSetDevice(d);
+      cur = d;
+    }
+  };
   ncclResult_t res = ncclSuccess;
   for (size_t k = 0; k < rounds && res == ncclSuccess; k++) {
     std::vector<Planned> planned;
     planned.reserve(order.size());
-    for (ncclComm* c : order) {
-      auto& v = perComm[c];
+    for (size_t j = 0; j < order.size(); j++) {
+      auto& v = perComm[j];
       if (k >= v.size()) continue;
-      Planned p;
-      res = planOp(ops[v[k]], &p);
+      planned.emplace_back();
+      res = planOp(ops[v[k]], &planned.back());
       if (res != ncclSuccess) break;
-      planned.push_back(p);
     }
     if (res != ncclSuccess) break;
-    // copies / no-ops
-    std::map<std::tuple<int, int, int, int>, std::vector<Planned*>> launches;
+    // copies / one-rank scaling run at once; kernels are fused per (device, type, op, protocol)
+    typedef std::tuple<int, int, int, int> LaunchKey;
+    std::vector<std::pair<LaunchKey, std::vector<Planned*>>> launches;
     for (auto& p : planned) {
       if (p.noop) continue;
-      hipSetDevice(p.op.comm->cudaDev);
+      setDev(p.op.comm->cudaDev);
       if (p.memcpyOnly) {
         if (hipMemcpyAsync(p.op.recvbuff, p.op.sendbuff, p.copyBytes, hipMemcpyDeviceToDevice, p.op.stream) != hipSuccess) {
           res = ncclUnhandledCudaError;
@@ -370,12 +385,16 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
         }
         continue;
       }
-      launches[std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto)].push_back(&p);
+      const LaunchKey key = std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto);
+      size_t j = 0;
+      while (j < launches.size() && launches[j].first != key) j++;
+      if (j == launches.size()) launches.emplace_back(key, std::vector<Planned*>());
+      launches[j].second.push_back(&p);
     }
     for (auto& kv : launches) {
       if (res != ncclSuccess) break;
       auto& list = kv.second;
-      hipSetDevice(std::get<0>(kv.first));
+      setDev(std::get<0>(kv.first));
       if (list.size() > (size_t)kMaxLaunchRanks) {
         // the ranks' workgroups wait on each other: launched in parts they could only time out
         WARN("MSCCL: %zu co-resident ranks on device %d in one group; one launch carries at most %d",
@@ -386,7 +405,7 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
       res = launchGroup(list);
     }
   }
-  hipSetDevice(saved);
+  setDev(saved);
   return res;
 }
 
