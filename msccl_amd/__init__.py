@@ -86,6 +86,7 @@ def lib() -> ctypes.CDLL:
     L.mscclAmdAlgoJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
     L.mscclAmdPlanJson.argtypes = [ctypes.c_char_p, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
     L.mscclAmdCommInfo.argtypes = [vp, ctypes.c_char_p, sz]
+    L.mscclAmdNpkitDump.argtypes = [vp, ctypes.c_char_p]
     L.mscclAmdBootstrapAllgather.argtypes = [ctypes.POINTER(UniqueId), i, i, vp, sz, vp]
     L.mscclAmdAlgoBlocks.argtypes = [vp, i]
     L.mscclAmdTraceRead.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
@@ -212,6 +213,11 @@ class Comm:
         buf = ctypes.create_string_buffer(1 << 16)
         _check(lib().mscclAmdCommInfo(self.handle, buf, len(buf)), "mscclAmdCommInfo")
         return json.loads(buf.value.decode())
+
+    def npkit_dump(self, directory: str = None) -> None:
+        """Write the NPKit dump now (MSCCL_AMD_NPKIT=1 at init; include/msccl_amd_npkit.h);
+        ncclCommDestroy writes it too, into $NPKIT_DUMP_DIR or /tmp/."""
+        _check(lib().mscclAmdNpkitDump(self.handle, directory.encode() if directory else None), "mscclAmdNpkitDump")
 
     def algo_blocks(self, idx: int) -> int:
         return lib().mscclAmdAlgoBlocks(self.handle, idx)

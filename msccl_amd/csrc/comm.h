@@ -87,6 +87,10 @@ struct ncclComm {
   uint64_t* dFlags = nullptr;
   msccl::TraceEvent* dTrace = nullptr;   // MSCCL_AMD_TRACE: [216 * maxSplit][traceEvents]
   int traceEvents = 0;
+  msccl::NpkitLog* dNpkit = nullptr;      // MSCCL_AMD_NPKIT (npkit.cc)
+  msccl::NpkitEvent* dNpkitEvents = nullptr;
+  uint64_t* dNpkitHeads = nullptr;
+  int npkitCap = 0, npkitClockKHz = 0;
   void* scratch = nullptr;
   size_t scratchSize = 0;
   uint32_t workIndex = 1;    // host launch counter (the device epoch drives the flags)
@@ -134,6 +138,11 @@ namespace msccl {
 ncclResult_t commSetupTransport(std::vector<ncclComm*>& comms, Bootstrap* boot);
 ncclResult_t commFree(ncclComm* comm, bool peerBarrier);
 bool commValid(const ncclComm* comm);
+
+// npkit.cc
+ncclResult_t npkitSetup(ncclComm* comm);
+ncclResult_t npkitDump(ncclComm* comm, const char* dir);  // dir null: $NPKIT_DUMP_DIR or /tmp/
+void npkitFree(ncclComm* comm);
 
 // transport.cc
 size_t tableIndex(int group, int chan, int peer, int nRanks);

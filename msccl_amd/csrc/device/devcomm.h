@@ -50,6 +50,21 @@ enum TraceType : uint16_t {
   kEvHeader = 0xFFFF
 };
 
+// NPKit-compatible event log (include/msccl_amd_npkit.h): 16-B events {type:8 | size:32 |
+// rsvd:24, timestamp} (npkit_struct.h:8-17), one buffer per thread block, kept across launches.
+struct NpkitEvent {
+  uint64_t bits;  // type | size << 8 | rsvd << 40
+  uint64_t ts;
+};
+struct NpkitLog {
+  NpkitEvent* events;    // [kNpkitDevBuffers][cap]
+  uint64_t* heads;       // [kNpkitDevBuffers] events written so far (may exceed cap: the rest dropped)
+  int64_t cpuOffsetNs;   // host system_clock ns = GPU clock ticks * nsPerTick + cpuOffsetNs
+  int32_t cap;
+  int32_t nsPerTick;     // s_memrealtime period (10 ns at 100 MHz)
+};
+constexpr int kNpkitDevBuffers = 216;  // MSCCL_MAX_NUM_THREAD_BLOCKS: buffer = thread block
+
 // LL FIFO line (ncclLLFifoLine, devcomm.h:35-48): two 8-B {4-B data, 4-B flag} granules.
 struct alignas(16) LLLine { uint32_t d0, f0, d1, f1; };
 
@@ -179,6 +194,7 @@ struct RankWork {
   int32_t traceEvents;
   int32_t redOpArgIsPtr;        // redOpArg is a device address of the scalar (ncclScalarDevice)
   uint64_t redOpArg;            // PreMulSum scale bits / SumPostDiv divisor (ncclDevRedOpFull::scalarArg)
+  NpkitLog* npkit;              // MSCCL_AMD_NPKIT (null = off)
 };
 
 struct LaunchArgs {
@@ -197,6 +213,9 @@ OneRankFn getOneRankFn(int dtype);
 constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = resident workgroups per CU
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
 LaunchFn getSmallLaunchFn(int dtype, int redop);  // mscclSmallKernel (LL, Sum..Min), or null
+// One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):
+// NPKit's host/GPU clock calibration.  Returns 0 on a successful launch.
+int launchClockProbe(uint64_t* hostWord, void* stream);
 
 }  // namespace msccl
 

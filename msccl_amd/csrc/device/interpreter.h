@@ -24,6 +24,7 @@
 // flag, and no transfer ever needs another workgroup's data.  A launch uses split = 1 whenever
 // a chunk is not a whole number of packs.
 #pragma once
+#include "msccl_amd_npkit.h"
 #include "primitives.h"
 
 namespace msccl {
@@ -99,6 +100,41 @@ struct Interp {
   int refNthreads;
   TraceEvent* trace;  // this workgroup's trace slot (null = tracing off)
   int nev, maxEv;
+  NpkitEvent* nkBuf;  // NPKit buffer of this thread block (null: off, or not the tb's sub 0)
+  uint64_t* nkHeadG;  // its persistent event count
+  uint64_t nkHead;
+  int nkCap;
+
+  // NPKit event (the reference's NpKit::CollectGpuEvent, npkit.h:26-37): thread 0 writes, every
+  // thread keeps the count so it stays uniform
+  __device__ __forceinline__ void nk(uint8_t type, uint64_t size, uint64_t ts) {
+    if (nkBuf != nullptr) {
+      if (tid == 0 && nkHead < (uint64_t)nkCap) {
+        NpkitEvent e;
+        e.bits = (uint64_t)type | ((size > 0xFFFFFFFFull ? 0xFFFFFFFFull : size) << 8);
+        e.ts = ts;
+        nkBuf[nkHead] = e;
+      }
+      nkHead++;
+    }
+  }
+  __device__ __forceinline__ void nk(uint8_t type, uint64_t size) {
+    if (nkBuf != nullptr) nk(type, size, __builtin_amdgcn_s_memrealtime());
+  }
+  // <primitive>_ENTRY of a transfer type (prims_ll.h:455-536; _EXIT = _ENTRY + 1)
+  static __device__ __forceinline__ uint8_t nkPrim(int type) {
+    switch (type) {
+      case tSend: return NPKIT_EVENT_SEND_ENTRY;
+      case tRecv: return NPKIT_EVENT_RECV_ENTRY;
+      case tRCS: return NPKIT_EVENT_RECV_COPY_SEND_ENTRY;
+      case tRRS: return NPKIT_EVENT_RECV_REDUCE_SEND_ENTRY;
+      case tRRC: return NPKIT_EVENT_RECV_REDUCE_COPY_ENTRY;
+      case tRRCS: return NPKIT_EVENT_RECV_REDUCE_COPY_SEND_ENTRY;
+      case tCpy: return NPKIT_EVENT_LOCAL_COPY_ENTRY;
+      case tCopySend: return NPKIT_EVENT_COPY_SEND_ENTRY;
+      default: return NPKIT_EVENT_REDUCE_ENTRY;
+    }
+  }
 
   __device__ __forceinline__ void ev(uint16_t type, uint16_t step, uint32_t arg) {
     if (trace != nullptr && tid == 0 && nev < maxEv) {
@@ -883,6 +919,18 @@ struct Interp {
     nev = 1;
     maxEv = w.traceEvents;
     ev(kEvSetup, 0, 0);
+    nkBuf = nullptr;
+    if (w.npkit != nullptr && sub == 0 && bid < kNpkitDevBuffers) {
+      // NPKIT_GPU_SYNC_TIME(bid, tid) (msccl_interpreter.h:88): the host time of this launch
+      // start, then the GPU clock it corresponds to
+      const NpkitLog* lg = w.npkit;
+      nkCap = lg->cap;
+      nkBuf = lg->events + (size_t)bid * nkCap;
+      nkHeadG = lg->heads + bid;
+      nkHead = uni(*nkHeadG);
+      nk(NPKIT_EVENT_TIME_SYNC_CPU, 0, (uint64_t)((int64_t)t0 * lg->nsPerTick + lg->cpuOffsetNs));
+      nk(NPKIT_EVENT_TIME_SYNC_GPU, 0, t0);
+    }
 
     T* thisInput = (T*)w.sendbuff;
     T* thisOutput = (T*)w.recvbuff;
@@ -956,7 +1004,9 @@ struct Interp {
       for (int i = 0; i < hd.nsteps; i++) {
         const DevTransfer t = loadTransfer(&tr[i]);
         if (t.numDeps > 0) {
+          nk(NPKIT_EVENT_DEP_CHECK_ENTRY, t.numDeps);
           waitDeps(t, flags, workIndex, iter, sub, maxSplit);
+          nk(NPKIT_EVENT_DEP_CHECK_EXIT, t.numDeps);
           step += t.numDeps - 1;
           ev(kEvDepWait, (uint16_t)i, 0);
         }
@@ -1015,10 +1065,12 @@ struct Interp {
             s.npk = thisCount * s.Lq;
           }
           ev(kEvPrimBegin, (uint16_t)i, ((uint32_t)t.type << 24) | (uint32_t)min(s.npk * PE, 0xFFFFFF));
+          nk(nkPrim(t.type), (uint64_t)s.n * TS);
           if (!exec(t, srcP, dstP, srcoff, dstoff, grid + (int64_t)c * sizePer, sizePer, s)) {
             stop = true;
             break;
           }
+          nk(nkPrim(t.type) + 1, (uint64_t)s.n * TS);
           if (t.type == tRe && c == 0) step += t.numReds - 1;
           ev(kEvPrimEnd, (uint16_t)i, 0);
         }
@@ -1028,6 +1080,7 @@ struct Interp {
       }
     }
     epilogue(w, bid, sub, workIndex);
+    if (nkBuf != nullptr && tid == 0) *nkHeadG = nkHead;
     ev(kEvEnd, 0, 0);
     if (trace != nullptr && tid == 0) {
       TraceEvent h;
@@ -1051,6 +1104,7 @@ struct Interp {
   __device__ __forceinline__ void runSmall(const RankWork& w, int local) {
     redArg = 0;
     trace = nullptr;
+    nkBuf = nullptr;
     const int split = w.split;
     const int lg = __builtin_ctz((unsigned)split);
     const int bid = local >> lg, sub = local & (split - 1);

@@ -152,6 +152,7 @@ RankWork makeRingWork(Planned& p) {
   w.llCleanMask = comm->llCleanMask;
   w.trace = comm->dTrace;
   w.traceEvents = comm->traceEvents;
+  w.npkit = comm->dNpkit;
   w.redOpArg = p.op.redArg;
   w.redOpArgIsPtr = p.op.redArgIsPtr;
   w.flags = comm->dFlags;
@@ -193,6 +194,7 @@ RankWork makeWork(Planned& p) {
   w.llCleanMask = comm->llCleanMask;
   w.trace = comm->dTrace;
   w.traceEvents = comm->traceEvents;
+  w.npkit = comm->dNpkit;
   w.redOpArg = p.op.redArg;
   w.redOpArgIsPtr = p.op.redArgIsPtr;
   w.flags = comm->dFlags;
@@ -248,12 +250,12 @@ RankWork makeWork(Planned& p) {
 }
 
 // mscclSmallKernel takes a call that is one LL interpreter iteration of an MSCCL schedule, run
-// untraced, with a Sum..Min op (interpreter.h: runSmall).  Both kernels cut a
+// without trace or NPKit log, with a Sum..Min op (interpreter.h: runSmall).  Both kernels cut a
 // transfer into the same primitive calls, so ranks that choose differently still agree.
 bool smallEligible(const Planned& p, const RankWork& w) {
   const ncclComm* comm = p.op.comm;
   return comm->knobs.smallKernel && p.plan.ringColl == 0 && p.plan.proto == kProtoLL && p.op.devOp <= 3 &&
-         p.plan.nIters == 1 && p.plan.sizePerChunk <= p.plan.chunkSize && w.trace == nullptr &&
+         p.plan.nIters == 1 && p.plan.sizePerChunk <= p.plan.chunkSize && w.trace == nullptr && w.npkit == nullptr &&
          (w.split & (w.split - 1)) == 0 &&
          p.plan.sizePerChunk * p.plan.nchunksPerLoop * refTypeSize(p.plan.dtype) <= (1ll << 30);
 }

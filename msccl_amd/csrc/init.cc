@@ -182,6 +182,7 @@ ncclResult_t commFinish(ncclComm* comm) {
     dc.trace = comm->dTrace;
     dc.traceEvents = comm->traceEvents;
   }
+  NCCLCHECK(npkitSetup(comm));
   dc.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
   dc.unused = nullptr;
   NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
@@ -285,6 +286,8 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
   if (comm->dComm) hipFree(comm->dComm);
   if (comm->dFlags) hipFree(comm->dFlags);
   if (comm->dTrace) hipFree(comm->dTrace);
+  if (comm->dNpkit && comm->dComm) npkitDump(comm, nullptr);  // NPKIT_TEARDOWN (npkit.h:214-219)
+  npkitFree(comm);
   if (comm->scratch) hipFree(comm->scratch);
   if (comm->boot && comm->ownsBoot) {
     if (peerBarrier) comm->boot->barrier();  // peers may still read our arena until everyone is done
