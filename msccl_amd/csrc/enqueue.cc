@@ -54,7 +54,9 @@ struct Planned {
   bool inPlace = false;
 };
 
-ncclResult_t planOp(const CollOp& op, Planned* out) {
+// asyncMany: the group holds more than one op of this communicator; under
+// MSCCL_AMD_REFERENCE_SELECTION such ops skip MSCCL as the reference's do (enqueue.cc:448-460).
+ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
   ncclComm* comm = op.comm;
   out->op = op;
   int ts = refTypeSize(op.dtype);
@@ -72,6 +74,10 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
     if (op.sendbuff == op.recvbuff) out->noop = true;
     return ncclSuccess;
   }
+  if (asyncMany && comm->knobs.referenceSelection && op.customAlgo >= 0) {
+    WARN("MSCCL algorithms is not supposed to be used in async mode!");  // enqueue.cc:448-451
+    return ncclInvalidUsage;
+  }
   CallDesc c;
   c.coll = op.coll;
   c.count = op.count;
@@ -82,7 +88,7 @@ ncclResult_t planOp(const CollOp& op, Planned* out) {
   c.inPlace = inPlaceOf(op.coll, op.sendbuff, op.recvbuff, op.count, op.dtype, comm->rank);
   c.customAlgo = op.customAlgo;
   out->inPlace = c.inPlace;
-  int idx = selectAlgo(comm->algos, comm->regs, c, comm->knobs);
+  int idx = asyncMany && comm->knobs.referenceSelection ? -1 : selectAlgo(comm->algos, comm->regs, c, comm->knobs);
   if (idx < 0) {
     // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
     if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
@@ -362,7 +368,7 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
       auto& v = perComm[j];
       if (k >= v.size()) continue;
       planned.emplace_back();
-      res = planOp(ops[v[k]], &planned.back());
+      res = planOp(ops[v[k]], &planned.back(), v.size() > 1);
       if (res != ncclSuccess) break;
     }
     if (res != ncclSuccess) break;

@@ -54,9 +54,13 @@ static int getNthreads(const char* env) {  // NCCL_PARAM-style cached read; -2 =
 Knobs Knobs::fromEnv() {
   Knobs k;
   memset(&k, 0, sizeof(k));
-  // The reference needs NCCL_ALGO to contain MSCCL for AllReduce (tuning.cc:186,217) because
-  // ring/tree exist next to it; here MSCCL is the primary algorithm, so it is on unless excluded.
-  k.mscclOn = listEnables(getenv("NCCL_ALGO"), "MSCCL", true);
+  // The reference runs an MSCCL AllReduce only when NCCL_ALGO lists MSCCL (algoEnable default 0,
+  // tuning.cc:186; zeroed AllReduce bandwidths, tuning.cc:217), and never when a group holds more
+  // than one op of the communicator (asyncOpCount > 1, enqueue.cc:448-460).  Here MSCCL is the
+  // primary algorithm: on unless NCCL_ALGO excludes it, in any group.
+  // MSCCL_AMD_REFERENCE_SELECTION=1 restores both reference rules.
+  k.referenceSelection = envInt("MSCCL_AMD_REFERENCE_SELECTION", 0) != 0;
+  k.mscclOn = listEnables(getenv("NCCL_ALGO"), "MSCCL", !k.referenceSelection);
   static const char* names[3] = {"LL", "LL128", "Simple"};
   for (int p = 0; p < 3; p++) k.protoOn[p] = listEnables(getenv("NCCL_PROTO"), names[p], true);
   k.nthreads = getNthreads("NCCL_NTHREADS");
@@ -103,7 +107,9 @@ static void argsCheck(const CallDesc& c, int64_t* count, int* dtype, int64_t* nB
 int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registration>& regs, const CallDesc& c,
                const Knobs& k) {
   if (!(c.redop == 0 || c.redop == 1 || c.redop == 2 || c.redop == 3)) return -1;  // tuning.cc:345
-  if (!k.mscclOn) return -1;
+  // NCCL_ALGO gates AllReduce only: "Only disable algo for Allreduce since others only have one"
+  // (tuning.cc:216-217)
+  if (!k.mscclOn && c.coll == kAllReduce) return -1;
   int64_t count, nBytes;
   int dt;
   argsCheck(c, &count, &dt, &nBytes);

@@ -67,6 +67,7 @@ struct Knobs {
   int32_t ringOn, treeOn;    // NCCL_ALGO enables Ring / Tree for the fallback (tuning.cc:188-197)
   int64_t treeMaxBytes;      // MSCCL_AMD_TREE_MAX_BYTES: AllReduce fallback calls up to this size take the tree
   int32_t smallKernel;       // MSCCL_AMD_SMALL_KERNEL: one-iteration LL launches take mscclSmallKernel
+  int32_t referenceSelection;  // MSCCL_AMD_REFERENCE_SELECTION: the reference's MSCCL gating (below)
   static Knobs fromEnv();
 };
 
