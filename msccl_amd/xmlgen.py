@@ -35,6 +35,13 @@ class _Tb:
         return self.add("nop", "i", -1, "o", -1, 0, depid, deps, 0)
 
 
+
+# Default maxBytes of the schedules that use scratch (two-phase all-pairs, one-shot): the runtime
+# allocates scratch for maxBytes at init (init.cc:809-835), so an unbounded default would pin the
+# 8 GiB MSCCL_AMD_MAX_SCRATCH cap per rank.  Larger calls take the fallback unless the caller
+# passes max_bytes.  Scratch-free schedules (pair one-shot, ring) stay unbounded.
+SCRATCH_SCHEDULE_MAX_BYTES = 1 << 30
+
 def _emit(name: str, proto: str, nchannels: int, ncpl: int, ngpus: int, coll: str, inplace: bool,
           gpus: Dict[int, Tuple[int, int, int, List[_Tb]]], min_bytes: Optional[int], max_bytes: Optional[int],
           nthreads: Optional[int] = None) -> str:
@@ -147,7 +154,7 @@ def allreduce_allpairs(n: int, instances: int = 1, proto: str = "LL", inplace: b
         tbs = list(red.values()) + list(ptb.values())
         gpus[r] = (ncpl, 0 if inplace else ncpl, I * (n - 1) * n, tbs)
     if max_bytes is None:
-        max_bytes = 1 << 62
+        max_bytes = SCRATCH_SCHEDULE_MAX_BYTES
     return _emit(name, proto, I, ncpl, n, "allreduce", inplace, gpus, min_bytes, max_bytes, nthreads)
 
 
@@ -203,7 +210,7 @@ def allreduce_oneshot(n: int, instances: int = 1, proto: str = "LL",
         tbs = red + [ptb[(k, p)] for p in peers for k in range(I)]
         gpus[r] = (I, 0, I * nslot, tbs)
     if max_bytes is None:
-        max_bytes = 1 << 62
+        max_bytes = SCRATCH_SCHEDULE_MAX_BYTES
     return _emit(name, proto, I, I, n, "allreduce", True, gpus, min_bytes, max_bytes, nthreads)
 
 
