@@ -484,6 +484,7 @@ def main():
             print("# %10d B  %9.2f us  algbw %8.2f  busbw %8.2f GB/s" % (nbytes, t * 1e6, algbw, bus),
                   file=sys.stderr, flush=True)
     head = results[-1]
+    headline_small = comms[0].info()["last"].get("small", 0) == 1  # which kernel the headline ran
     # roofline of the dominant (largest) launch
     ranks_on_gpu = 1 if multi else n
     kernel_s = head["kernel_ms"] / 1e3
@@ -496,7 +497,7 @@ def main():
                      "payload_achieved counts them at payload size.  The launch's buffers (%d MiB, plus "
                      "FIFO slots) fit the 256 MB MALL, whose hits FETCH_SIZE counts: traffic is "
                      "memory-side bytes, not HBM-array bytes" % (head["bytes"] * ranks_on_gpu >> 20)),
-            "kernel": "mscclKernel<%s,Sum,%s>" % (dtname, a.proto),
+            "kernel": "%s<%s,Sum,%s>" % ("mscclSmallKernel" if headline_small else "mscclKernel", dtname, a.proto),
             "algorithmic_bytes_per_launch": head["hbm_bytes_per_rank"] * ranks_on_gpu,
             "kernel_ms": head["kernel_ms"]}
     if multi:

@@ -1093,14 +1093,15 @@ struct Interp {
   }
 
   // ---------------------------------------------------------------- small calls
-  // A launch whose every rank's call is one interpreter iteration (sizePerChunk <= chunkSize),
-  // outside the ring / tree fallback and without tracing (enqueue.cc: smallEligible).  Then
-  // grid = 0, nelem = sizePerChunk and the iteration needs no chunk arithmetic; every offset
-  // fits 32 bits and split is a power of two, so a workgroup's positions are shifts.  The
-  // transfers, their cut into calls (the same macT rule as run(), so each end of a connection
-  // may run either kernel) and the primitives are run()'s; what goes is the 64-bit iteration
-  // arithmetic and most of the scalar state the big loop keeps live (SGPR spills), which for a
-  // call of a few KiB is most of a launch.
+  // A launch whose every rank's call runs run()'s loop as equal passes: one iteration
+  // (sizePerChunk <= chunkSize) or full iterations merged `merge` at a time with nothing left
+  // over (enqueue.cc: smallEligible), outside the ring / tree fallback and without tracing.
+  // Then every pass has nelem = min(sizePerChunk, chunkSize * merge) and needs no chunk
+  // arithmetic, offsets fit 32 bits and split is a power of two, so a workgroup's
+  // positions are shifts.  The transfers, their cut into calls (run()'s macT and reach rules, so
+  // each end of a connection may run either kernel), the flags (iter = pass) and the primitives
+  // are run()'s; what goes is the 64-bit iteration arithmetic and most of the scalar state the
+  // big loop keeps live (SGPR spills), a few us per launch.
   __device__ __forceinline__ void runSmall(const RankWork& w, int local) {
     redArg = 0;
     trace = nullptr;
@@ -1112,46 +1113,61 @@ struct Interp {
     const uint64_t workIndex = prologue(w, bid, sub, hd);
     const int maxSplit = w.maxSplit;
     T* const bufs[3] = {(T*)w.sendbuff, (T*)w.recvbuff, (T*)w.scratch};
-    const int nelem = (int)w.sizePerChunk;
+    // element offsets stay below 2^30 (smallEligible: at most 1 GiB per buffer), so 32 bits
+    const int sizePer = (int)w.sizePerChunk;
+    const int chunk = (int)w.chunkSize;
+    const int nelem = sizePer <= chunk ? sizePer : min(sizePer, chunk * (int)w.merge);
+    const bool whole = nelem == sizePer;  // run()'s `nelem == sizePer`
     const int mac = w.maxAllowedCount;
     const int64_t maxOp = w.maxOpElems;
     const uint32_t Qc = ((uint32_t)nelem + PE - 1) / PE;
     const int q0 = (int)((Qc * (uint32_t)sub) >> lg), q1 = (int)((Qc * (uint32_t)(sub + 1)) >> lg);
-    int step = 0;
-    for (int i = 0; i < hd.nsteps; i++) {
-      const DevTransfer t = loadTransfer(&tr[i]);
-      if (t.numDeps > 0) {
-        waitDeps(t, w.flags, workIndex, 0, sub, maxSplit);
-        step += t.numDeps - 1;
-      }
-      T* srcP = bufs[t.srcbuf < 2 ? t.srcbuf : 2];
-      T* dstP = bufs[t.dstbuf < 2 ? t.dstbuf : 2];
-      const int macT = (t.type != tRe && (int64_t)nelem * t.count <= maxOp) ? t.count : mac;
-      bool stop = false;
-      for (int c = 0; c < t.count; c += macT) {
-        const int thisCount = macT < t.count - c ? macT : t.count - c;
-        Shape s;
-        s.n = nelem * thisCount;
-        if (split == 1) {
-          s.Q = (s.n + PE - 1) / PE;
-          s.q0 = 0;
-          s.Lq = s.Q;
-          s.npk = s.Q;
-        } else {
-          s.Q = (int)Qc;
-          s.q0 = q0;
-          s.Lq = q1 - q0;
-          s.npk = thisCount * s.Lq;
+    // one pass: grid = offset of the pass, iter = its index; false when a transfer ends the tb
+    auto runPass = [&](int grid, int iter) __attribute__((always_inline)) -> bool {
+      int step = 0;
+      for (int i = 0; i < hd.nsteps; i++) {
+        const DevTransfer t = loadTransfer(&tr[i]);
+        if (t.numDeps > 0) {
+          waitDeps(t, w.flags, workIndex, iter, sub, maxSplit);
+          step += t.numDeps - 1;
         }
-        if (!exec(t, srcP, dstP, (t.srcoff + c) * nelem, (t.dstoff + c) * nelem, c * nelem, nelem, s)) {
-          stop = true;
-          break;
+        T* srcP = bufs[t.srcbuf < 2 ? t.srcbuf : 2];
+        T* dstP = bufs[t.dstbuf < 2 ? t.dstbuf : 2];
+        int macT = (t.type != tRe && whole && (int64_t)nelem * t.count <= maxOp) ? t.count : mac;
+        if ((int64_t)nelem * TS * macT > (int64_t)0x7fffff00) {  // run()'s descriptor-reach cut
+          const int64_t reach = (int64_t)0x7fffff00 / ((int64_t)nelem * TS);
+          macT = reach < 1 ? 1 : (int)reach;
         }
-        if (t.type == tRe && c == 0) step += t.numReds - 1;
+        for (int c = 0; c < t.count; c += macT) {
+          const int thisCount = macT < t.count - c ? macT : t.count - c;
+          Shape s;
+          s.n = nelem * thisCount;
+          if (split == 1) {
+            s.Q = (s.n + PE - 1) / PE;
+            s.q0 = 0;
+            s.Lq = s.Q;
+            s.npk = s.Q;
+          } else {
+            s.Q = (int)Qc;
+            s.q0 = q0;
+            s.Lq = q1 - q0;
+            s.npk = thisCount * s.Lq;
+          }
+          if (!exec(t, srcP, dstP, grid + (t.srcoff + c) * sizePer, grid + (t.dstoff + c) * sizePer,
+                    grid + c * sizePer, sizePer, s))
+            return false;
+          if (t.type == tRe && c == 0) step += t.numReds - 1;
+        }
+        if (t.hasDep) publishFlag(w.flags, bid * maxSplit + sub, workIndex, iter, step);
+        step++;
       }
-      if (stop) break;
-      if (t.hasDep) publishFlag(w.flags, bid * maxSplit + sub, workIndex, 0, step);
-      step++;
+      return true;
+    };
+    if (whole) {
+      runPass(0, 0);  // the common small call: no pass loop state
+    } else {
+      for (int grid = 0, iter = 0; grid < sizePer; grid += nelem, iter++)
+        if (!runPass(grid, iter)) break;
     }
     epilogue(w, bid, sub, workIndex);
   }

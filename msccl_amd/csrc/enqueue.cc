@@ -255,15 +255,22 @@ RankWork makeWork(Planned& p) {
   return w;
 }
 
-// mscclSmallKernel takes a call that is one LL interpreter iteration of an MSCCL schedule, run
-// without trace or NPKit log, with a Sum..Min op (interpreter.h: runSmall).  Both kernels cut a
+// mscclSmallKernel takes a call whose LL interpreter loop runs in equal passes (one iteration,
+// or full iterations merged with none left over) of an MSCCL schedule, without trace or NPKit
+// log, with a Sum..Min op (interpreter.h: runSmall).  Both kernels cut a
 // transfer into the same primitive calls, so ranks that choose differently still agree.
 bool smallEligible(const Planned& p, const RankWork& w) {
   const ncclComm* comm = p.op.comm;
+  // run()'s loop in equal passes: a single iteration, or full iterations merged `merge` at a
+  // time with none left over (interpreter.h: run, runSmall)
+  const int64_t sp = p.plan.sizePerChunk, cs = p.plan.chunkSize;
+  const int64_t k = cs > 0 ? sp / cs : 0, m = std::min<int64_t>(std::max<int>(1, w.merge), std::max<int64_t>(1, k));
+  const bool onePass = sp <= cs || (cs > 0 && sp % cs == 0 && k % m == 0);
   return comm->knobs.smallKernel && p.plan.ringColl == 0 && p.plan.proto == kProtoLL && p.op.devOp <= 3 &&
-         p.plan.nIters == 1 && p.plan.sizePerChunk <= p.plan.chunkSize && w.trace == nullptr && w.npkit == nullptr &&
+         onePass && w.trace == nullptr && w.npkit == nullptr &&
          (w.split & (w.split - 1)) == 0 &&
-         p.plan.sizePerChunk * p.plan.nchunksPerLoop * refTypeSize(p.plan.dtype) <= (1ll << 30);
+         p.plan.sizePerChunk * std::max<int64_t>(p.plan.nchunksPerLoop, comm->algos[p.plan.algoIndex].nScratchChunks) *
+                 refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit element offsets
 }
 
 ncclResult_t launchGroup(std::vector<Planned*>& ps) {

@@ -50,7 +50,10 @@ def test_small_kernel_matches_oracle_and_general(name, count, dt, op, tmp_path, 
         monkeypatch.setenv("MSCCL_AMD_SMALL_KERNEL", small)
         with CoResident(n, [xml], str(tmp_path)) as cr:
             ins, got, last = _run(cr, count, dt, op, seed=11)
-            assert all(l["small"] == int(small == "1" and one_iter) for l in last), last
+            if small == "0":
+                assert all(l["small"] == 0 for l in last), last
+            elif one_iter:  # several iterations may still run as one merged pass (small too)
+                assert all(l["small"] == 1 for l in last), last
             want, idx = cr.oracle(L.ALLREDUCE, count, dt, op, ins, True)
             assert idx == 0
             for r in range(n):
@@ -61,15 +64,34 @@ def test_small_kernel_matches_oracle_and_general(name, count, dt, op, tmp_path, 
         assert np.array_equal(outs["1"][r].view(np.uint8), outs["0"][r].view(np.uint8))
 
 
-def test_large_call_takes_general_kernel(tmp_path, monkeypatch):
-    """Several interpreter iterations: the general kernel runs (and still matches the oracle)."""
+def test_partial_last_iteration_takes_general_kernel(tmp_path, monkeypatch):
+    """A partial last iteration (passes of unequal size): the general kernel runs (and still
+    matches the oracle)."""
     monkeypatch.setenv("MSCCL_AMD_SMALL_KERNEL", "1")
     xml = xmlgen.allreduce_pair_oneshot(1, "LL")
     with CoResident(2, [xml], str(tmp_path)) as cr:
-        count = 1 << 20
+        count = (1 << 20) + 64
         ins, got, last = _run(cr, count, 7, 0, seed=3)
         assert all(l["small"] == 0 for l in last), last
         want, _ = cr.oracle(L.ALLREDUCE, count, 7, 0, ins, True)
+        for r in range(2):
+            assert np.array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+
+
+@pytest.mark.parametrize("count", [1 << 16, 1 << 17, 1 << 19])
+def test_merged_pass_takes_small_kernel(tmp_path, monkeypatch, count):
+    """Full iterations merged into equal passes (8, 16 and 64 LL iterations of the 16-instance
+    pair schedule, the bench's 4, 8 and 32 MiB points; 64 runs as two passes of 32): the small
+    kernel, bit-equal to the oracle."""
+    monkeypatch.setenv("MSCCL_AMD_SMALL_KERNEL", "1")
+    xml = xmlgen.allreduce_pair_oneshot(16, "LL")
+    xp = tmp_path / "p.xml"
+    xp.write_text(xml)
+    assert M.plan_json(str(xp), 0, 2, L.ALLREDUCE, count * 16, 7, 0, True)["nIters"] > 1
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        ins, got, last = _run(cr, count * 16, 7, 0, seed=5)
+        assert all(l["small"] == 1 for l in last), last
+        want, _ = cr.oracle(L.ALLREDUCE, count * 16, 7, 0, ins, True)
         for r in range(2):
             assert np.array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
 

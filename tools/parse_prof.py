@@ -36,7 +36,7 @@ def find(d, pattern):
 
 
 def is_msccl(name):
-    return "mscclKernel" in name
+    return "mscclKernel" in name or "mscclSmallKernel" in name
 
 
 def counter_avg(d, counter):
@@ -81,7 +81,7 @@ def main():
     res["write_size_kib_avg"], res["write_launches"] = write, nw
     if fetch is not None and write is not None:
         res["traffic_bytes_per_launch"] = (2.0 * fetch + write) * 1024.0
-        res["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 per mscclKernel dispatch (gfx950 FETCH_SIZE correction)"
+        res["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 per interpreter-kernel dispatch (gfx950 FETCH_SIZE correction)"
     kt = os.path.join(out, "kt.json")
     if os.path.exists(kt):
         try:
