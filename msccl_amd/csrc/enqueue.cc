@@ -259,6 +259,12 @@ RankWork makeWork(Planned& p) {
 // or full iterations merged with none left over) of an MSCCL schedule, without trace or NPKit
 // log, with a Sum..Min op (interpreter.h: runSmall).  Both kernels cut a
 // transfer into the same primitive calls, so ranks that choose differently still agree.
+// chunks any transfer offset of the algorithm can reach (the loader bounds offsets by the
+// buffers' chunk counts, topo.cc:725)
+int64_t maxChunkIndex(const Algorithm& a, int64_t ncpl) {
+  return std::max<int64_t>({ncpl, (int64_t)a.nInputChunks, (int64_t)a.nOutputChunks, (int64_t)a.nScratchChunks});
+}
+
 bool smallEligible(const Planned& p, const RankWork& w) {
   const ncclComm* comm = p.op.comm;
   // run()'s loop in equal passes: a single iteration, or full iterations merged `merge` at a
@@ -269,7 +275,7 @@ bool smallEligible(const Planned& p, const RankWork& w) {
   return comm->knobs.smallKernel && p.plan.ringColl == 0 && p.plan.proto == kProtoLL && p.op.devOp <= 3 &&
          onePass && w.trace == nullptr && w.npkit == nullptr &&
          (w.split & (w.split - 1)) == 0 &&
-         p.plan.sizePerChunk * std::max<int64_t>(p.plan.nchunksPerLoop, comm->algos[p.plan.algoIndex].nScratchChunks) *
+         p.plan.sizePerChunk * maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop) *
                  refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit element offsets
 }
 
