@@ -214,10 +214,12 @@ RankWork makeWork(Planned& p) {
   int split = comm->algoSplit.empty() ? 1 : comm->algoSplit[p.plan.algoIndex];
   const int64_t pe = 16 / refTypeSize(p.plan.dtype);
   if (p.plan.sizePerChunk % pe != 0) split = 1;
-  // Small messages: fewer, fuller workgroups (at least one pack per lane of every workgroup);
-  // a split forced with MSCCL_AMD_SPLIT is kept as is.
+  // Small messages: fewer, fuller workgroups, at least one pack per 4 lanes of every workgroup
+  // (C2 pair schedule: 128 KiB 9.4 -> 8.4 us, 512 KiB 9.6 -> 8.9 us against one pack per lane;
+  // below that more workgroups only add launch and poll overhead); a split forced with
+  // MSCCL_AMD_SPLIT is kept as is.
   if (comm->knobs.split <= 0)
-    while (split > 1 && p.plan.sizePerChunk / pe < (int64_t)split * kNT) split /= 2;
+    while (split > 1 && p.plan.sizePerChunk / pe < (int64_t)split * (kNT / 4)) split /= 2;
   w.split = (uint8_t)split;
   w.nBlocks = (int16_t)(da.nBlocks * split);
   // Consecutive full interpreter iterations can run as one: every element still sees the same
