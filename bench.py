@@ -57,17 +57,23 @@ def parse():
     return ap.parse_args()
 
 
-def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only: bool = False):
+def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only: bool = False, fused=()):
     """Algorithmic HBM bytes and wire bytes of one launch for one rank (whole schedule).
-    payload_only counts FIFO traffic at its payload size (LL flags / LL128 flag words excluded)."""
+    payload_only counts FIFO traffic at its payload size (LL flags / LL128 flag words excluded).
+    fused: thread blocks whose s + rrc exchange ran fused (comm info "algoFuse"): the rrc reuses
+    the source the s read, one read of B less."""
     f = 1.0 if payload_only else {0: 2.0, 1: 4.0 / 3.0}.get(proto, 1.0)  # LL: 8 B data per 16-B line
     hbm = wire = 0
-    for tb in algo["tbs"]:
+    for b_i, tb in enumerate(algo["tbs"]):
+        first_s = b_i in fused and proto == 0
         for t in tb["transfers"]:
             typ, cnt, nred = t[0], t[5], t[10]
             b = cnt * size_per * ts
             if typ == 0:      # s
                 hbm += b + f * b; wire += f * b
+                if first_s:
+                    hbm -= b
+                    first_s = False
             elif typ == 1:    # r
                 hbm += f * b + b
             elif typ == 2:    # rcs
@@ -395,6 +401,7 @@ def main():
     maxb = max(sizes)
     bufs = [torch.empty(maxb // 4 + 64, dtype=torch.float32, device=d).uniform_(-1, 1) for d in devs]
     algos = {t[3]: M.algo_json(t[3], my_ranks[0], n) for t in tiers}
+    fused = {t[3]: set(f) for t, f in zip(tiers, comms[0].info().get("algoFuse", []))}
 
     def one_step(nbytes):
         cnt = nbytes // ts
@@ -472,8 +479,8 @@ def main():
         bus = algbw * 2 * (n - 1) / n
         algo = algos[tier[3]]
         size_per = cnt // ncpl
-        hbm, wire = schedule_bytes(algo, size_per, ts, proto_id)
-        payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True)
+        hbm, wire = schedule_bytes(algo, size_per, ts, proto_id, fused=fused.get(tier[3], ()))
+        payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True, fused=fused.get(tier[3], ()))
         ok = verify(nbytes)
         verified.append(ok)
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),

@@ -37,7 +37,11 @@ enum BufId : uint8_t { kInput = 0, kOutput = 1, kScratch = 2 };
 enum OpType : uint8_t {
   kSend = 0, kRecv = 1, kRecvCopySend = 2, kRecvReduceSend = 3, kRecvReduceCopy = 4,
   kRecvReduceCopySend = 5, kLocalCopy = 6, kReduce = 7, kResAdd = 8,
-  kCopySend = 9  // ring AllGather out of place (directCopySend, all_gather.h:59); never from XML
+  kCopySend = 9,  // ring AllGather out of place (directCopySend, all_gather.h:59); never from XML
+  // `s` fused with the `rrc` that follows it (same source chunks, same peer): the device image of
+  // a thread block whose exchange both ends run as one pass (transport.cc: fusableTbs); never
+  // from XML
+  kSendRecvReduceCopy = 10
 };
 
 // Device reduction ops (ncclDevRedOp_t, devcomm.h): Sum, Prod, Max, Min, PreMulSum, SumPostDiv

@@ -49,6 +49,13 @@ struct DevAlgoHost {
   int connSplit = 1;
 };
 
+// A thread block whose exchange with its single peer may run fused (transport.cc: fusableTbs):
+// tb index, index of its `s` (the `rrc` follows), channel, peer.
+struct FuseCandidate {
+  int16_t tb, index, chan, peer;
+};
+constexpr int kMaxFuse = 64;  // candidates per algorithm exchanged at init
+
 struct ncclCommImpl;
 }  // namespace msccl
 
@@ -66,6 +73,8 @@ struct ncclComm {
   std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
   std::vector<int> algoSendRun;    // per algorithm: longest run of send chunks before a receive, max over
                                    // every rank's program (same on all ranks)
+  std::vector<std::vector<msccl::FuseCandidate>> algoFuse;  // per algorithm: thread blocks running fused
+                                                            // (both ends of the exchange agreed at init)
   int maxSplit = 1;                // sub-connections per (channel, peer)
   int coResident = 1;              // ranks of this communicator on this rank's GPU
 
@@ -151,6 +160,7 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
                               const std::vector<char*>& peerBases, const std::vector<int>& peerRemote);
 ncclResult_t algoUpload(ncclComm* comm);
 int algoSendRunOf(const Algorithm& a);
+std::vector<FuseCandidate> fusableTbs(const Algorithm& a);
 ncclResult_t ringUpload(ncclComm* comm);
 
 // enqueue.cc

@@ -90,6 +90,12 @@ int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
   for (size_t i = 0; i < comm->algoSplit.size(); i++) o << (i ? "," : "") << comm->algoSplit[i];
   o << "],\"algoSendRun\":[";
   for (size_t i = 0; i < comm->algoSendRun.size(); i++) o << (i ? "," : "") << comm->algoSendRun[i];
+  o << "],\"algoFuse\":[";  // per algorithm: thread blocks whose s + rrc exchange runs fused
+  for (size_t i = 0; i < comm->algoFuse.size(); i++) {
+    o << (i ? "," : "") << "[";
+    for (size_t j = 0; j < comm->algoFuse[i].size(); j++) o << (j ? "," : "") << comm->algoFuse[i][j].tb;
+    o << "]";
+  }
   const auto& L = comm->last;
   o << "],\"last\":{\"algo\":" << L.algo << ",\"proto\":" << L.proto << ",\"split\":" << L.split
     << ",\"merge\":" << L.merge << ",\"ringColl\":" << L.ringColl << ",\"ringChannels\":" << L.ringChannels

@@ -29,7 +29,8 @@
 
 namespace msccl {
 
-enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7, tCopySend = 9 };
+enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7, tCopySend = 9,
+             tSendRrc = 10 /* s fused with the rrc after it (transport.cc: fusableTbs) */ };
 enum : int { pLL = 0, pLL128 = 1, pSimple = 2 };
 
 struct alignas(16) BlockShared {
@@ -128,7 +129,8 @@ struct Interp {
       case tRecv: return NPKIT_EVENT_RECV_ENTRY;
       case tRCS: return NPKIT_EVENT_RECV_COPY_SEND_ENTRY;
       case tRRS: return NPKIT_EVENT_RECV_REDUCE_SEND_ENTRY;
-      case tRRC: return NPKIT_EVENT_RECV_REDUCE_COPY_ENTRY;
+      case tRRC:
+      case tSendRrc: return NPKIT_EVENT_RECV_REDUCE_COPY_ENTRY;
       case tRRCS: return NPKIT_EVENT_RECV_REDUCE_COPY_SEND_ENTRY;
       case tCpy: return NPKIT_EVENT_LOCAL_COPY_ENTRY;
       case tCopySend: return NPKIT_EVENT_COPY_SEND_ENTRY;
@@ -263,7 +265,9 @@ struct Interp {
   static __device__ __forceinline__ int l16LineIdx(int u, int j) { return ((u >> 6) << 8) + (j << 6) + (u & 63); }
   static __device__ __forceinline__ int l16Lines(int nv) { return nv == 3 ? 4 : nv + 1; }  // lines for nv packs
 
-  template <int RECV, int SEND, int SRC, int DST>
+  // FUSED (tSendRrc, RECV = SEND = SRC = DST = 1): send the source, receive the peer's same step,
+  // dst = fn(peer, source): the s and rrc of one exchange in one pass over the source.
+  template <int RECV, int SEND, int SRC, int DST, int FUSED = 0>
   __device__ void llOp(const T* src, T* dst, const Shape s) {
     constexpr int E = 8 / TS;  // elements per LL line
     const int nlinesFull = (s.n + E - 1) / E;
@@ -290,7 +294,7 @@ struct Interp {
       if constexpr (kL16) {
         l16Step<RECV, SEND, SRC, DST>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1);
       } else {
-        llStep<RECV, SEND, SRC, DST>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1, nlinesFull);
+        llStep<RECV, SEND, SRC, DST, FUSED>(srs, drs, frs, rslot, rflag, sflag, vec, s, s0, s1, nlinesFull);
       }
       if (SEND) {
         if ((sendStep & llCleanMask) == llCleanMask) {
@@ -317,6 +321,114 @@ struct Interp {
       }
       s0 = s1;
     } while (s0 < s.npk);
+  }
+
+  // ---------------------------------------------------------------- fused exchange (tSendRrc, LL)
+  // The s and rrc of one exchange (transport.cc: fusableTbs), the send one FIFO step ahead of the
+  // receive.  Iteration k issues together the source loads of send step k + 1 and the line polls
+  // of receive step k, then stores fn(peer, source) of step k, whose source is still in
+  // registers from iteration k - 1, and the lines of step k + 1.  One memory round trip per step
+  // and the source is read once: 6 S HBM bytes per rank for the pair exchange instead of 7 S.
+  // Steps are cut as llOp cuts the s and the rrc (one pass per step: slotPacks <= kNT * U), so
+  // the peer may run either form.
+  // packs of FIFO step j of a call: B = op pack, act = in this step, two = second line used
+  __device__ __forceinline__ void llStepPacks(const Shape& s, int slotPacks, int nlinesFull, int j, int (&B)[U],
+                                              bool (&act)[U], bool (&two)[U]) {
+    const int s0 = j * slotPacks, n = min(s.npk - s0, slotPacks);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int q = tid + u * kNT;
+      act[u] = q < n;
+      B[u] = act[u] ? s.bufPack(s0 + q) : 0;
+      two[u] = act[u] && 2 * B[u] + 1 < nlinesFull;
+    }
+  }
+  // lines of one send step (pack q of the step -> llLineIdx(q, h)), then LL cleanup and the step
+  __device__ __forceinline__ void llSendLines(const Shape& s, int slotLines, int nlinesFull, int s0, int s1,
+                                              const bool (&act)[U], const bool (&two)[U], const u32x4 (&v)[U]) {
+    const __amdgpu_buffer_rsrc_t frs = makeRsrc(sc->ll + (sendStep % kLLFifoSlots) * (uint64_t)slotLines);
+    const uint32_t sflag = (uint32_t)(sendStep + 1) & llFlagMask;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (!act[u]) continue;
+      const int q = tid + u * kNT;
+      st16<kAuxFifo>(frs, (uint32_t)llLineIdx(q, 0) * 16, (u32x4){v[u].x, sflag, v[u].y, sflag});
+      if (two[u]) st16<kAuxFifo>(frs, (uint32_t)llLineIdx(q, 1) * 16, (u32x4){v[u].z, sflag, v[u].w, sflag});
+    }
+    if ((sendStep & llCleanMask) == llCleanMask) {  // prims_ll.h:90-97, as in llOp
+      for (int l = tid; l < slotLines; l += kNT) {
+        const int q = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
+        const bool used = s0 + q < s1 && 2 * s.bufPack(s0 + q) + h < nlinesFull;
+        if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, sflag, 0, sflag});
+      }
+    }
+    sendStep++;
+  }
+
+  __device__ void llFusedOp(const T* src, T* dst, const Shape s) {
+    const int slotLines = uni(sc->llSlotLines);
+    const int slotPacks = slotLines / 2;
+    if (slotPacks > kNT * U) {  // several passes per step (NCCL_LL_BUFFSIZE raised): lockstep form
+      [[clang::always_inline]] llOp<1, 1, 1, 1, 1>(src, dst, s);
+      return;
+    }
+    constexpr int E = 8 / TS;
+    const int nlinesFull = (s.n + E - 1) / E;
+    const __amdgpu_buffer_rsrc_t srs = makeRsrc(src), drs = makeRsrc(dst);
+    const bool vec = aligned16(src) && aligned16(dst);
+    const int nsteps = s.npk > slotPacks ? (s.npk + slotPacks - 1) / slotPacks : 1;  // llOp: >= 1 step
+    int B[U];
+    bool act[U], two[U];
+    u32x4 v[U];  // source of the step being received
+    waitSendCredit<kLLFifoSlots>();
+    llStepPacks(s, slotPacks, nlinesFull, 0, B, act, two);
+#pragma unroll
+    for (int u = 0; u < U; u++) v[u] = act[u] ? loadPack(srs, vec, B[u], s.n) : (u32x4){0, 0, 0, 0};
+    llSendLines(s, slotLines, nlinesFull, 0, min(s.npk, slotPacks), act, two, v);
+    for (int k = 0; k < nsteps; k++) {
+      const int j = k + 1;
+      const bool snd = j < nsteps;
+      int Bs[U];
+      bool as[U], ts[U];
+      u32x4 vs[U];
+      if (snd) {
+        waitSendCredit<kLLFifoSlots>();
+        llStepPacks(s, slotPacks, nlinesFull, j, Bs, as, ts);
+#pragma unroll
+        for (int u = 0; u < U; u++) vs[u] = as[u] ? loadPack(srs, vec, Bs[u], s.n) : (u32x4){0, 0, 0, 0};
+      }
+      llStepPacks(s, slotPacks, nlinesFull, k, B, act, two);
+      const LLLine* rslot = rc->ll + (recvStep % kLLFifoSlots) * (uint64_t)slotLines;
+      const uint32_t rflag = (uint32_t)(recvStep + 1) & llFlagMask;
+      const void* la[2 * U];
+      u32x4 ln[2 * U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int q = tid + u * kNT;
+        la[2 * u] = act[u] ? rslot + llLineIdx(q, 0) : rslot;
+        la[2 * u + 1] = two[u] ? rslot + llLineIdx(q, 1) : la[2 * u];
+      }
+      ldLines8(la, ln);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        Spin spins;
+        while (act[u] && (ln[2 * u].y != rflag || ln[2 * u].w != rflag || ln[2 * u + 1].y != rflag ||
+                          ln[2 * u + 1].w != rflag)) {
+          if (spinAbort(spins)) break;
+          ldLines2(la[2 * u], la[2 * u + 1], ln[2 * u], ln[2 * u + 1]);
+        }
+        const u32x4 peer = {ln[2 * u].x, ln[2 * u].z, ln[2 * u + 1].x, ln[2 * u + 1].z};
+        if (act[u]) storePack(drs, vec, B[u], s.n, F::pack(peer, v[u]));  // rrc: fn(peer, local)
+      }
+      recvStep++;
+      __syncthreads();
+      if (tid == 0) atomicStoreSys(rc->remoteHead, recvStep);
+      if (snd) {
+        llSendLines(s, slotLines, nlinesFull, j * slotPacks, min(s.npk, (j + 1) * slotPacks), as, ts, vs);
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = vs[u];
+      }
+    }
   }
 
   // ---------------------------------------------------------------- LL128, 1/2/4-byte types
@@ -472,7 +584,7 @@ struct Interp {
 
   // one LL step: packs [s0, s1) of the call, U packs per lane per pass with all their loads and
   // line polls in flight together
-  template <int RECV, int SEND, int SRC, int DST>
+  template <int RECV, int SEND, int SRC, int DST, int FUSED>
   __device__ void llStep(__amdgpu_buffer_rsrc_t srs, __amdgpu_buffer_rsrc_t drs,
                                          __amdgpu_buffer_rsrc_t frs, LLLine* rslot, uint32_t rflag,
                                          uint32_t sflag, bool vec, const Shape& s, int s0, int s1, int nlinesFull) {
@@ -496,6 +608,17 @@ struct Interp {
         if constexpr (PP::kPre) {
 #pragma unroll
           for (int u = 0; u < U; u++) v[u] = PP::pre(v[u], redArg);
+        }
+      }
+      if (FUSED) {
+        // the source goes out before this lane waits for the peer's lines: the peer's wait for
+        // this step never depends on this workgroup's progress
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          if (!act[u]) continue;
+          const int q = base + u * kNT;
+          st16<kAuxFifo>(frs, (uint32_t)llLineIdx(q, 0) * 16, (u32x4){v[u].x, sflag, v[u].y, sflag});
+          if (two[u]) st16<kAuxFifo>(frs, (uint32_t)llLineIdx(q, 1) * 16, (u32x4){v[u].z, sflag, v[u].w, sflag});
         }
       }
       if (RECV) {
@@ -526,7 +649,7 @@ struct Interp {
           for (int u = 0; u < U; u++) v[u] = PP::post(v[u], redArg);
         }
       }
-      if (SEND) {
+      if (SEND && !FUSED) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
           if (!act[u]) continue;
@@ -868,6 +991,7 @@ struct Interp {
 
   // One primitive call of transfer t; false for MSCCL_RES_ADD / unknown types (the tb ends,
   // msccl_interpreter.h:195-196).  `reOff` is the chunk offset of a fused reduction's sources.
+  template <bool FUSE>
   __device__ __forceinline__ bool exec(const DevTransfer& t, T* srcP, T* dstP, int64_t srcoff, int64_t dstoff,
                                        int64_t reOff, int64_t sizePer, const Shape& s) {
     switch (t.type) {
@@ -879,6 +1003,12 @@ struct Interp {
       case tRRCS: op<1, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
       case tCpy: localCopy(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
       case tCopySend: op<0, 1, 1, 1>(srcP + srcoff, dstP + dstoff, s); __syncthreads(); break;
+      case tSendRrc:  // LL only (run / runSmall turn it into tSend otherwise); dst from the rrc
+        if constexpr (FUSE && PROTO == pLL && OP <= 3) {  // MSCCL schedules run Sum..Min only
+          // inlined like the other primitive calls (a call frame costs scratch and SGPR spills)
+          [[clang::always_inline]] llFusedOp(srcP + srcoff, dstP + dstoff, s);
+        }
+        break;
       case tRe: reduce(srcP, red + t.redPtr, reOff, sizePer, t.numReds, dstP + dstoff, s); __syncthreads(); break;
       default: return false;
     }
@@ -891,6 +1021,16 @@ struct Interp {
     raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
     __builtin_memcpy(&t, &raw, sizeof(t));
     return t;
+  }
+
+  // a tSendRrc transfer runs fused with LL in mscclSmallKernel (FUSE) when both FIFO slot sizes
+  // agree (the two ends then cut the same steps); otherwise, and always in the general kernel
+  // (trace, NPKit, uneven passes: its register budget has no room for the fused pipeline), as
+  // its s followed by its rrc, which a fused peer interoperates with (transport.cc: fusableTbs)
+  template <bool FUSE>
+  __device__ __forceinline__ bool fuseable(const DevTransfer& t) const {
+    if constexpr (!FUSE || PROTO != pLL || OP > 3) return false;
+    return t.type == tSendRrc && uni(sc->llSlotLines) == uni(rc->llSlotLines);
   }
 
   __device__ __forceinline__ void publishFlag(uint64_t* flags, int slot, uint64_t workIndex, uint64_t iter, int step) {
@@ -1002,7 +1142,10 @@ struct Interp {
       const int q0 = (int)divNonNeg((int64_t)Qc * sub, split), q1 = (int)divNonNeg((int64_t)Qc * (sub + 1), split);
       int step = 0;
       for (int i = 0; i < hd.nsteps; i++) {
-        const DevTransfer t = loadTransfer(&tr[i]);
+        DevTransfer t = loadTransfer(&tr[i]);
+        const bool fused = fuseable<false>(t);
+        if (t.type == tSendRrc && !fused) t.type = tSend;
+        const DevTransfer td = fused ? loadTransfer(&tr[i + 1]) : t;  // the rrc: output buffer
         if (t.numDeps > 0) {
           nk(NPKIT_EVENT_DEP_CHECK_ENTRY, t.numDeps);
           waitDeps(t, flags, workIndex, iter, sub, maxSplit);
@@ -1011,7 +1154,7 @@ struct Interp {
           ev(kEvDepWait, (uint16_t)i, 0);
         }
         T* srcP = t.srcbuf == 0 ? thisInput : (t.srcbuf == 1 ? thisOutput : thisScratch);
-        T* dstP = t.dstbuf == 0 ? thisInput : (t.dstbuf == 1 ? thisOutput : thisScratch);
+        T* dstP = td.dstbuf == 0 ? thisInput : (td.dstbuf == 1 ? thisOutput : thisScratch);
         // maxAllowedCount keeps one reference primitive call within one FIFO step
         // (enqueue.cc:700-711); these primitives cut calls into FIFO steps themselves, so when the
         // iteration covers whole chunks (consecutive chunks are contiguous) a transfer's chunks
@@ -1031,7 +1174,7 @@ struct Interp {
         }
         for (int c = 0; c < t.count; c += macT) {
           int64_t srcoff = grid + (int64_t)(t.srcoff + c) * sizePer;
-          int64_t dstoff = grid + (int64_t)(t.dstoff + c) * sizePer;
+          int64_t dstoff = grid + (int64_t)(td.dstoff + c) * sizePer;
           const int thisCount = macT < t.count - c ? macT : t.count - c;
           Shape s;
           s.n = nelem * thisCount;
@@ -1066,7 +1209,7 @@ struct Interp {
           }
           ev(kEvPrimBegin, (uint16_t)i, ((uint32_t)t.type << 24) | (uint32_t)min(s.npk * PE, 0xFFFFFF));
           nk(nkPrim(t.type), (uint64_t)s.n * TS);
-          if (!exec(t, srcP, dstP, srcoff, dstoff, grid + (int64_t)c * sizePer, sizePer, s)) {
+          if (!exec<false>(t, srcP, dstP, srcoff, dstoff, grid + (int64_t)c * sizePer, sizePer, s)) {
             stop = true;
             break;
           }
@@ -1075,6 +1218,11 @@ struct Interp {
           ev(kEvPrimEnd, (uint16_t)i, 0);
         }
         if (stop) break;
+        if (fused) {  // the s published nothing (fusableTbs); the rrc's flag below
+          step++;
+          i++;
+          t = td;
+        }
         if (t.hasDep) publishFlag(flags, slot, workIndex, iter, step);
         step++;
       }
@@ -1126,13 +1274,16 @@ struct Interp {
     auto runPass = [&](int grid, int iter) __attribute__((always_inline)) -> bool {
       int step = 0;
       for (int i = 0; i < hd.nsteps; i++) {
-        const DevTransfer t = loadTransfer(&tr[i]);
+        DevTransfer t = loadTransfer(&tr[i]);
+        const bool fused = fuseable<true>(t);
+        if (t.type == tSendRrc && !fused) t.type = tSend;
+        const DevTransfer td = fused ? loadTransfer(&tr[i + 1]) : t;
         if (t.numDeps > 0) {
           waitDeps(t, w.flags, workIndex, iter, sub, maxSplit);
           step += t.numDeps - 1;
         }
         T* srcP = bufs[t.srcbuf < 2 ? t.srcbuf : 2];
-        T* dstP = bufs[t.dstbuf < 2 ? t.dstbuf : 2];
+        T* dstP = bufs[td.dstbuf < 2 ? td.dstbuf : 2];
         int macT = (t.type != tRe && whole && (int64_t)nelem * t.count <= maxOp) ? t.count : mac;
         if ((int64_t)nelem * TS * macT > (int64_t)0x7fffff00) {  // run()'s descriptor-reach cut
           const int64_t reach = (int64_t)0x7fffff00 / ((int64_t)nelem * TS);
@@ -1153,10 +1304,15 @@ struct Interp {
             s.Lq = q1 - q0;
             s.npk = thisCount * s.Lq;
           }
-          if (!exec(t, srcP, dstP, grid + (t.srcoff + c) * sizePer, grid + (t.dstoff + c) * sizePer,
+          if (!exec<true>(t, srcP, dstP, grid + (t.srcoff + c) * sizePer, grid + (td.dstoff + c) * sizePer,
                     grid + c * sizePer, sizePer, s))
             return false;
           if (t.type == tRe && c == 0) step += t.numReds - 1;
+        }
+        if (fused) {
+          step++;
+          i++;
+          t = td;
         }
         if (t.hasDep) publishFlag(w.flags, bid * maxSplit + sub, workIndex, iter, step);
         step++;

@@ -100,6 +100,8 @@ struct SplitRecord {
   int32_t nAlgos;
   int32_t nBlocks[kMaxAlgos];
   int32_t sendRun[kMaxAlgos];
+  int32_t nFuse[kMaxAlgos];
+  int16_t fuse[kMaxAlgos][kMaxFuse][2];  // (channel, peer) of each fusable exchange (fusableTbs)
   Knobs knobs;
 };
 
@@ -113,6 +115,12 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) {
     s.nBlocks[a] = comm->algos[a].nBlocks;
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
+    const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
+    for (size_t i = 0; i < fc.size() && s.nFuse[a] < kMaxFuse; i++) {
+      s.fuse[a][s.nFuse[a]][0] = fc[i].chan;
+      s.fuse[a][s.nFuse[a]][1] = fc[i].peer;
+      s.nFuse[a]++;
+    }
   }
   s.knobs = comm->knobs;
   s.knobs.smallKernel = 0;  // a rank-local choice: both kernels cut the same FIFO steps
@@ -157,6 +165,20 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs);
     comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
+  }
+  // an exchange runs fused only when both ends offered it (fusableTbs)
+  comm->algoFuse.assign(comm->algos.size(), {});
+  for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos && comm->knobs.fuse; a++) {
+    auto offered = [&](int rank, int chan, int peer) {
+      const SplitRecord& r = recs[rank];
+      if ((int)a >= r.nAlgos) return false;
+      for (int i = 0; i < r.nFuse[a]; i++)
+        if (r.fuse[a][i][0] == chan && r.fuse[a][i][1] == peer) return true;
+      return false;
+    };
+    for (const FuseCandidate& f : fusableTbs(comm->algos[a]))
+      if (f.peer < (int)recs.size() && offered(comm->rank, f.chan, f.peer) && offered(f.peer, f.chan, comm->rank))
+        comm->algoFuse[a].push_back(f);
   }
   INFO(kSubInit, "rank %d: %d co-resident ranks per GPU (max), %d sub-connections per connection", comm->rank,
        maxCo, comm->maxSplit);

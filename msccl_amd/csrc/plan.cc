@@ -78,6 +78,7 @@ Knobs Knobs::fromEnv() {
   k.treeOn = listEnables(getenv("NCCL_ALGO"), "Tree", true);
   k.treeMaxBytes = envInt("MSCCL_AMD_TREE_MAX_BYTES", -1);  // -1: 16 KiB per rank (makeRingPlan)
   k.smallKernel = envInt("MSCCL_AMD_SMALL_KERNEL", 1) != 0;
+  k.fuse = envInt("MSCCL_AMD_FUSE", 1) != 0;
   return k;
 }
 

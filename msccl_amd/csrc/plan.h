@@ -68,6 +68,8 @@ struct Knobs {
   int64_t treeMaxBytes;      // MSCCL_AMD_TREE_MAX_BYTES: AllReduce fallback calls up to this size take the tree
   int32_t smallKernel;       // MSCCL_AMD_SMALL_KERNEL: one-iteration LL launches take mscclSmallKernel
   int32_t referenceSelection;  // MSCCL_AMD_REFERENCE_SELECTION: the reference's MSCCL gating (below)
+  int32_t fuse;              // MSCCL_AMD_FUSE: fused s + rrc exchanges (transport.cc: fusableTbs)
+  int32_t pad;               // no implicit padding (Knobs are compared with memcmp)
   static Knobs fromEnv();
 };
 

@@ -423,6 +423,33 @@ int algoSendRunOf(const Algorithm& a) {
   return best;
 }
 
+// Thread blocks whose first FIFO transfers are `s` then `rrc` of the same source chunks with a
+// single peer (send peer == receive peer), with no flag published after the send and no wait
+// before the receive.  When the peer's thread block on that connection has the same shape, the
+// two ends exchange in lockstep: each FIFO step is sent, then the peer's same step is received
+// and reduced with the values just sent, so the source is read once (LL: 7 S -> 6 S HBM bytes per
+// rank for the pair exchange).  Each receive waits only for a step its peer sends before waiting
+// itself, so the fused pair cannot deadlock, and an end that runs the pair unfused (s fully,
+// then rrc) still makes progress against a fused one.  Values are those of s then rrc: the same
+// fn(peer, local) per element (interpreter.h: llStep FUSED).
+std::vector<FuseCandidate> fusableTbs(const Algorithm& a) {
+  std::vector<FuseCandidate> out;
+  auto fifo = [](uint8_t t) { return t <= kRecvReduceCopySend || t == kCopySend; };
+  for (int b = 0; b < a.nBlocks; b++) {
+    const ThreadBlock& tb = a.tbs[b];
+    if (tb.sendpeer < 0 || tb.sendpeer != tb.recvpeer) continue;
+    const std::vector<Transfer>& ts = tb.transfers;
+    size_t i = 0;
+    while (i < ts.size() && !fifo(ts[i].type)) i++;
+    if (i + 1 >= ts.size()) continue;
+    const Transfer &s = ts[i], &r = ts[i + 1];
+    if (s.type == kSend && r.type == kRecvReduceCopy && s.srcbuf == r.srcbuf && s.srcoff == r.srcoff &&
+        s.count == r.count && s.hasDep == 0 && r.numDeps == 0)
+      out.push_back({(int16_t)b, (int16_t)i, (int16_t)tb.channel, tb.sendpeer});
+  }
+  return out;
+}
+
 // Pack every algorithm's per-tb programs into fixed-stride images and upload them (replaces
 // the 29 MB mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 ncclResult_t algoUpload(ncclComm* comm) {
@@ -447,7 +474,11 @@ ncclResult_t algoUpload(ncclComm* comm) {
       h.nsteps = tb.nsteps;
       h.ndeps = (uint16_t)tb.depBid.size();
       h.nreds = (uint16_t)tb.redSrcOff.size();
-      putImage(img, (size_t)b * stride, h, tb.transfers, tb.depBid, tb.depStep, tb.redSrcOff);
+      std::vector<Transfer> ts = tb.transfers;
+      if (g < comm->algoFuse.size())
+        for (const FuseCandidate& f : comm->algoFuse[g])
+          if (f.tb == b) ts[f.index].type = kSendRecvReduceCopy;
+      putImage(img, (size_t)b * stride, h, ts, tb.depBid, tb.depStep, tb.redSrcOff);
     }
     NCCLCHECK(uploadImages(img, &d));
   }

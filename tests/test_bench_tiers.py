@@ -41,3 +41,18 @@ def test_tier_spec_with_kinds(bench, tmp_path):
     tiers = bench.make_xmls(2, "LL", 16, str(tmp_path), "0:4096:1:o,4096:65536:2:O,65536:1073741825:4")
     assert [t[4] for t in tiers] == ["o", "O", "a"]
     assert [t[2] for t in tiers] == [1, 2, 4]
+
+
+def test_fused_pair_exchange_bytes(bench, tmp_path):
+    """The roofline's algorithmic bytes: the pair exchange moves 7 S HBM bytes per rank unfused
+    (s: S + 2S of LL lines, rrc: 2S + S + S) and 6 S when its s + rrc run fused (the source is
+    read once; comm info "algoFuse" names the fused thread blocks)."""
+    p = tmp_path / "pair.xml"
+    p.write_text(bench.xmlgen.allreduce_pair_oneshot(16, "LL"))
+    algo = M.algo_json(str(p), 0, 2)
+    size_per, ts = 1 << 16, 4
+    S = 16 * size_per * ts
+    assert bench.schedule_bytes(algo, size_per, ts, 0)[0] == 7 * S
+    assert bench.schedule_bytes(algo, size_per, ts, 0, fused=set(range(16)))[0] == 6 * S
+    assert bench.schedule_bytes(algo, size_per, ts, 0, payload_only=True, fused=set(range(16)))[0] == 4 * S
+    assert bench.schedule_bytes(algo, size_per, ts, 2, fused=set(range(16)))[0] == 5 * S  # Simple: not fused

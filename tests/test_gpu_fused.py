@@ -1,0 +1,160 @@
+"""Fused s + rrc exchanges (transport.cc: fusableTbs, interpreter.h: llFusedOp).
+
+A thread block whose first FIFO transfers are `s` then `rrc` of the same source chunks with one
+peer runs both as one pass over its source when the peer's thread block on that connection has
+the same shape (agreed at init).  The values must stay those of s then rrc (the oracle's), for
+every size, type, op, in and out of place; both ends must agree before fusing (an asymmetric
+exchange would deadlock fused); and a fused rank must interoperate with an unfused one."""
+import os
+
+import numpy as np
+import pytest
+
+import msccl_amd as M
+from msccl_amd import xmlgen
+from msccl_amd.xmlgen import _Tb, _emit
+from oracle import loader as L
+from tests.gpu_harness import CoResident, describe_mismatch, gen_inputs, run_collective, to_torch
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
+
+
+def _check(got, want, what):
+    for r in range(len(want)):
+        assert np.array_equal(np.asarray(got[r]).view(np.uint8), np.asarray(want[r]).view(np.uint8)), \
+            "%s rank %d: %s" % (what, r, describe_mismatch(got[r], want[r]))
+
+
+def test_pair_exchange_is_fused_and_allpairs_is_not(tmp_path, monkeypatch):
+    monkeypatch.delenv("MSCCL_AMD_FUSE", raising=False)
+    with CoResident(2, [xmlgen.allreduce_pair_oneshot(4, "LL"), xmlgen.allreduce_allpairs(2, 2, "LL")],
+                    str(tmp_path)) as cr:
+        for c in cr.comms:
+            assert c.info()["algoFuse"] == [[0, 1, 2, 3], []], c.info()["algoFuse"]
+    monkeypatch.setenv("MSCCL_AMD_FUSE", "0")
+    with CoResident(2, [xmlgen.allreduce_pair_oneshot(4, "LL")], str(tmp_path)) as cr:
+        assert all(c.info()["algoFuse"] == [[]] for c in cr.comms)
+
+
+# counts: one pack per lane and less, one FIFO step per workgroup, several steps per pass (the
+# pipeline's steady state: 1 << 20 with one instance is 4 steps in each of 4 passes), a call that
+# is not whole packs (split 1, element tails), the bench's 4 and 32 MiB points
+@pytest.mark.parametrize("inst,count,dt,op", [
+    (1, 32, 7, 0), (1, 3000, 7, 0), (1, 1 << 16, 7, 0), (1, 1 << 20, 7, 0), (16, 1 << 20, 7, 0),
+    (16, 1 << 23, 7, 0),
+    (4, 1 << 18, 6, 0), (4, 1 << 18, 9, 0), (2, 100003 * 2, 6, 2), (4, 1 << 18, 2, 1), (1, 12345, 0, 0),
+    (2, 1 << 17, 8, 3),
+])
+def test_fused_matches_oracle_and_unfused(inst, count, dt, op, tmp_path, monkeypatch):
+    xml = xmlgen.allreduce_pair_oneshot(inst, "LL")
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MSCCL_AMD_FUSE", fuse)
+        got, want, _ = run_collective(xml, 2, L.ALLREDUCE, count, dt, op, True, seed=4, tmpdir=str(tmp_path))
+        _check(got, want, "fuse=%s" % fuse)
+        res[fuse] = got
+    _check(res["1"], res["0"], "fused vs unfused")
+
+
+@pytest.mark.parametrize("count", [4096, 1 << 18])
+def test_fused_out_of_place(count, tmp_path):
+    xml = xmlgen.allreduce_pair_oneshot(4, "LL", inplace=False)
+    got, want, _ = run_collective(xml, 2, L.ALLREDUCE, count, 7, 0, False, seed=8, tmpdir=str(tmp_path))
+    _check(got, want, "out of place")
+
+
+def test_fused_across_ll_cleanup(tmp_path, monkeypatch):
+    """MSCCL_AMD_TEST_LL_CLEANUP (8-bit flags, cleanup 8 steps in every 128): 24 launches of 16
+    fused FIFO steps per workgroup cross the flag wrap and several cleanup steps; Max is
+    idempotent, so the repeated in-place result stays the oracle's."""
+    monkeypatch.setenv("MSCCL_AMD_TEST_LL_CLEANUP", "1")
+    xml = xmlgen.allreduce_pair_oneshot(1, "LL")
+    got, want, _ = run_collective(xml, 2, L.ALLREDUCE, 1 << 20, 7, 2, True, seed=6, iters=24,
+                                  tmpdir=str(tmp_path))
+    _check(got, want, "cleanup")
+
+
+def _asymmetric_xml() -> str:
+    """2 ranks, one chunk: rank 0 sends then receives (a fusable shape), rank 1 receives, reduces
+    and only then sends.  Run fused on rank 0 alone, a call of more than one FIFO step would
+    deadlock (rank 0 waits for a step rank 1 sends only after receiving all of rank 0's)."""
+    gpus = {}
+    t0 = _Tb(0, 1, 1, 0)
+    t0.add("s", "i", 0, "i", 0, 1)
+    t0.add("rrc", "i", 0, "i", 0, 1)
+    gpus[0] = (1, 0, 0, [t0])
+    t1 = _Tb(0, 0, 0, 0)
+    t1.add("rrc", "i", 0, "i", 0, 1)
+    t1.add("s", "i", 0, "i", 0, 1)
+    gpus[1] = (1, 0, 0, [t1])
+    return _emit("asym", "LL", 1, 1, 2, "allreduce", True, gpus, 0, 1 << 40, None)
+
+
+def test_asymmetric_exchange_is_not_fused(tmp_path):
+    xml = _asymmetric_xml()
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        assert all(c.info()["algoFuse"] == [[]] for c in cr.comms)
+    got, want, _ = run_collective(xml, 2, L.ALLREDUCE, 1 << 21, 7, 0, True, seed=2, tmpdir=str(tmp_path))
+    _check(got, want, "asymmetric")
+
+
+def _mixed_proc(rank, world, xml_path, count, small, q_in, q_out):
+    import torch
+    os.environ["MSCCL_XML_FILES"] = xml_path
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "30"
+    os.environ["MSCCL_AMD_SMALL_KERNEL"] = small
+    torch.cuda.set_device(0)
+    uid = M.get_unique_id() if rank == 0 else None
+    if rank == 0:
+        for _ in range(world - 1):
+            q_in.put(uid)
+    else:
+        uid = q_in.get(timeout=60)
+    x = gen_inputs(world, count, 7, 9)[rank]
+    comm = M.Comm.init_rank(world, uid, rank)
+    t = to_torch(x, torch.device("cuda:0"))
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        comm.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, s)
+    torch.cuda.synchronize()
+    info = comm.info()
+    out = t.cpu().numpy()
+    err = comm.async_error()
+    comm.destroy()
+    q_out.put((rank, err, info["last"]["small"], info["algoFuse"], out))
+
+
+def test_fused_rank_interoperates_with_unfused_rank(tmp_path):
+    """Rank 0 runs mscclSmallKernel (fused exchange), rank 1 the general kernel (s, then rrc):
+    several FIFO steps per call, the values are the oracle's."""
+    import torch.multiprocessing as mp
+    from oracle import plan as P, sim as S
+    world, count = 2, 1 << 20
+    xml = xmlgen.allreduce_pair_oneshot(1, "LL")
+    p = tmp_path / "pair.xml"
+    p.write_text(xml)
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_mixed_proc, args=(r, world, str(p), count, "1" if r == 0 else "0", q_in, q_out))
+          for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, small, fuse, out = q_out.get(timeout=300)
+        res[r] = (err, small, fuse, out)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert res[0][1] == 1 and res[1][1] == 0, (res[0][1], res[1][1])
+    assert res[0][2] == [[0]] and res[1][2] == [[0]]
+    algos = [L.parse_xml(xml, r, world) for r in range(world)]
+    call = P.Call(L.ALLREDUCE, count, 7, 0, world, 0, True)
+    plan = P.make_plan([algos[0]], call, 0)
+    ins = gen_inputs(world, count, 7, 9)
+    for _ in range(3):
+        ins, _st = S.run(algos, plan, ins, [None] * world, L.ALLREDUCE, True)
+    for r in range(world):
+        assert res[r][0] == 0
+        assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
