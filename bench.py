@@ -403,11 +403,14 @@ def main():
     algos = {t[3]: M.algo_json(t[3], my_ranks[0], n) for t in tiers}
     fused = {t[3]: set(f) for t, f in zip(tiers, comms[0].info().get("algoFuse", []))}
 
+    ptrs = [b.data_ptr() for b in bufs]
+    sh = stream.cuda_stream
+
     def one_step(nbytes):
         cnt = nbytes // ts
         with M.group():
-            for c, b in zip(comms, bufs):
-                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+            for c, p in zip(comms, ptrs):
+                c.all_reduce(p, p, cnt, dt, M.SUM, sh)
 
     def pattern(r, cnt, dev):
         # exact small integers (|x| <= 4): every partial sum of up to 8 ranks is exact in every

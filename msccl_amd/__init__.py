@@ -162,6 +162,9 @@ class Comm:
 
     def __init__(self, handle: int):
         self.handle = ctypes.c_void_p(handle)
+        L = lib()
+        # the collective entry points, looked up once: they sit on the per-call path
+        self._ar, self._rs, self._ag = L.ncclAllReduce, L.ncclReduceScatter, L.ncclAllGather
 
     # ---- creation -------------------------------------------------------------------------
     @staticmethod
@@ -254,13 +257,19 @@ class Comm:
 
     # ---- collectives (pointers are device addresses, stream a hipStream_t or 0) ------------
     def all_reduce(self, send: int, recv: int, count: int, dtype: int, op: int = SUM, stream: int = 0) -> None:
-        _check(lib().ncclAllReduce(send, recv, count, dtype, op, self.handle, stream), "ncclAllReduce")
+        rc = self._ar(send, recv, count, dtype, op, self.handle, stream)
+        if rc:
+            raise NcclError(rc, "ncclAllReduce")
 
     def reduce_scatter(self, send: int, recv: int, recvcount: int, dtype: int, op: int = SUM, stream: int = 0) -> None:
-        _check(lib().ncclReduceScatter(send, recv, recvcount, dtype, op, self.handle, stream), "ncclReduceScatter")
+        rc = self._rs(send, recv, recvcount, dtype, op, self.handle, stream)
+        if rc:
+            raise NcclError(rc, "ncclReduceScatter")
 
     def all_gather(self, send: int, recv: int, sendcount: int, dtype: int, stream: int = 0) -> None:
-        _check(lib().ncclAllGather(send, recv, sendcount, dtype, self.handle, stream), "ncclAllGather")
+        rc = self._ag(send, recv, sendcount, dtype, self.handle, stream)
+        if rc:
+            raise NcclError(rc, "ncclAllGather")
 
     def all_to_all(self, send: int, recv: int, count: int, dtype: int, stream: int = 0) -> None:
         _check(lib().ncclAllToAll(send, recv, count, dtype, self.handle, stream), "ncclAllToAll")
@@ -276,11 +285,15 @@ class group:
     __slots__ = ()
 
     def __enter__(self):
-        _check(lib().ncclGroupStart(), "ncclGroupStart")
+        rc = lib().ncclGroupStart()
+        if rc:
+            raise NcclError(rc, "ncclGroupStart")
         return self
 
     def __exit__(self, *exc):
-        _check(lib().ncclGroupEnd(), "ncclGroupEnd")
+        rc = lib().ncclGroupEnd()
+        if rc:
+            raise NcclError(rc, "ncclGroupEnd")
         return False
 
 

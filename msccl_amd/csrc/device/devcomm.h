@@ -197,11 +197,17 @@ struct RankWork {
   NpkitLog* npkit;              // MSCCL_AMD_NPKIT (null = off)
 };
 
-struct LaunchArgs {
+template <int R>
+struct LaunchArgsN {
   int32_t nRanks;
   int32_t pad;
-  RankWork w[kMaxLaunchRanks];
+  RankWork w[R];
 };
+using LaunchArgs = LaunchArgsN<kMaxLaunchRanks>;
+// A launch of at most two ranks (one rank per process, or the 2-rank co-resident C2 launch) takes
+// a kernel whose argument block holds two RankWorks (424 B instead of 3.3 KiB): the HIP runtime
+// copies the whole block per launch, about 0.9 us more for the larger one (tools/host_lat).
+constexpr int kCompactLaunchRanks = 2;
 
 // Error codes in DevComm::errWord
 enum : uint32_t { kDevOk = 0, kDevTimeout = 1, kDevAbort = 2, kDevBadOp = 3 };

@@ -1344,8 +1344,8 @@ __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
 
 // Small-call variant (Interp::runSmall): every RankWork of the launch is one interpreter
 // iteration of an MSCCL schedule.
-template <typename T, int OP, int PROTO>
-__global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgs args) {
+template <typename T, int OP, int PROTO, int R>
+__global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> args) {
   __shared__ BlockShared sh;
   int b = blockIdx.x;
   int r = 0;

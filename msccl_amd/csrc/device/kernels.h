@@ -19,15 +19,29 @@ int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-// the small-call kernel (mscclSmallKernel, LL): same contract as launchKernel
+// the small-call kernel (mscclSmallKernel, LL): same contract as launchKernel; launches of at
+// most kCompactLaunchRanks ranks take the variant with the compact argument block
 template <typename T, int OP, int PROTO>
 int launchSmallKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  constexpr int RC = kCompactLaunchRanks;
   if (gridBlocks == kQueryResidency) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclSmallKernel<T, OP, PROTO>, kNT, 0) != hipSuccess) return 0;
-    return n;
+    int n = 0, m = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclSmallKernel<T, OP, PROTO, kMaxLaunchRanks>, kNT, 0) !=
+            hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, mscclSmallKernel<T, OP, PROTO, RC>, kNT, 0) != hipSuccess)
+      return 0;
+    return n < m ? n : m;
   }
-  hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, args);
+  if (args.nRanks <= RC) {
+    LaunchArgsN<RC> a;
+    a.nRanks = args.nRanks;
+    a.pad = 0;
+    for (int r = 0; r < RC; r++) a.w[r] = args.w[r];
+    hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO, RC>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO, kMaxLaunchRanks>), dim3(gridBlocks), dim3(kNT), 0,
+                       (hipStream_t)stream, args);
+  }
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 

@@ -291,10 +291,27 @@ def allreduce_ring(n: int, channels: int = 1, proto: str = "Simple", inplace: bo
 def reduce_scatter_allpairs(n: int, instances: int = 1, proto: str = "Simple", inplace: bool = False,
                             min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
                             nthreads: Optional[int] = None, name: str = "reduce_scatter_pairs") -> str:
-    """All-pairs ReduceScatter.  Input = n blocks of I chunks (block p -> rank p), output = I chunks."""
+    """All-pairs ReduceScatter.  Input = n blocks of I chunks (block p -> rank p), output = I chunks.
+    n > 2: every peer's copy lands in scratch (one thread block per peer, all links at once) and a
+    reduce thread block folds them.  n == 2: thread block k sends the peer's chunk and receives its
+    own with `rrc` (reduce with the local chunk, write the output): no scratch and no `re`, 5 B of
+    HBM traffic per output byte instead of 7 B."""
     I = instances
     ncpl = n * I
     gpus = {}
+    if n == 2:
+        for r in range(2):
+            p = 1 - r
+            tbs = []
+            for k in range(I):
+                tb = _Tb(k, p, p, k)
+                tb.add("s", "i", p * I + k, "o", k, 1)
+                tb.add("rrc", "i", r * I + k, "o", k, 1)
+                tbs.append(tb)
+            gpus[r] = (ncpl, I, 0, tbs)
+        if max_bytes is None:
+            max_bytes = 1 << 62
+        return _emit(name, proto, I, ncpl, n, "reduce_scatter", inplace, gpus, min_bytes, max_bytes, nthreads)
     for r in range(n):
         peers = [p for p in range(n) if p != r]
         slot = {p: i for i, p in enumerate(peers)}

@@ -106,6 +106,16 @@ def test_reduce_scatter(proto, inplace):
           inplace=inplace)
 
 
+@pytest.mark.parametrize("proto,inplace", [("Simple", False), ("Simple", True), ("LL", True), ("LL", False),
+                                           ("LL128", False)])
+@pytest.mark.parametrize("dt,count", [(7, 16 * 50001), (6, 4 * 1000 + 4), (9, 16 << 16), (2, 3 * 7)])
+def test_reduce_scatter_two_ranks(proto, inplace, dt, count):
+    """The 2-rank ReduceScatter (s of the peer's chunk, rrc of the own one: no scratch)."""
+    inst = 4 if count % 4 == 0 else 1
+    check(xmlgen.reduce_scatter_allpairs(2, inst, proto, inplace=inplace), 2, L.REDUCE_SCATTER, count, dt,
+          inplace=inplace)
+
+
 @pytest.mark.parametrize("proto,inplace", [("Simple", False), ("LL", True), ("LL", False), ("LL128", True)])
 def test_all_gather(proto, inplace):
     check(xmlgen.allgather_allpairs(8, 2, proto, inplace=inplace), 8, L.ALLGATHER, 2 * 33333, 7, inplace=inplace)

@@ -14,6 +14,8 @@
 #include "nccl.h"
 
 __global__ void emptyKernel(int) {}
+struct BigArgs { char b[4000]; };
+__global__ void emptyBigKernel(BigArgs) {}  // the interpreter's kernel-argument size
 
 static double now() {
   timespec t;
@@ -70,6 +72,18 @@ int main(int argc, char** argv) {
   hipStreamSynchronize(s);
   hipEventElapsedTime(&ms, e0, e1);
   printf("empty kernel: host %.2f us per launch, stream %.2f us per launch\n", host * 1e6, ms * 1e3 / iters);
+  BigArgs big = {};
+  for (int i = 0; i < 50; i++) hipLaunchKernelGGL(emptyBigKernel, dim3(1), dim3(64), 0, s, big);
+  hipStreamSynchronize(s);
+  hipEventRecord(e0, s);
+  t0 = now();
+  for (int i = 0; i < iters; i++) hipLaunchKernelGGL(emptyBigKernel, dim3(1), dim3(64), 0, s, big);
+  host = (now() - t0) / iters;
+  hipEventRecord(e1, s);
+  hipStreamSynchronize(s);
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("empty kernel, 4000-B arguments: host %.2f us per launch, stream %.2f us per launch\n", host * 1e6,
+         ms * 1e3 / iters);
   for (auto c : comms) ncclCommDestroy(c);
   return 0;
 }
