@@ -158,3 +158,15 @@ def test_fused_rank_interoperates_with_unfused_rank(tmp_path):
     for r in range(world):
         assert res[r][0] == 0
         assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
+
+
+@pytest.mark.parametrize("proto,count,dt", [("LL128", 1 << 18, 7), ("LL128", 3000, 6), ("Simple", 1 << 20, 9),
+                                            ("Simple", 12345, 7)])
+def test_fusable_image_on_other_protocols(proto, count, dt, tmp_path):
+    """The pair exchange's image carries the fused transfer type whatever the protocol; LL128 and
+    Simple run it as its s followed by its rrc, with the oracle's values."""
+    xml = xmlgen.allreduce_pair_oneshot(4 if count % 4 == 0 else 1, proto)
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        assert all(len(c.info()["algoFuse"][0]) > 0 for c in cr.comms)
+    got, want, _ = run_collective(xml, 2, L.ALLREDUCE, count, dt, 0, True, seed=12, tmpdir=str(tmp_path))
+    _check(got, want, proto)
