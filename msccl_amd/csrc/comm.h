@@ -96,6 +96,7 @@ struct ncclComm {
   uint64_t* dFlags = nullptr;
   msccl::TraceEvent* dTrace = nullptr;   // MSCCL_AMD_TRACE: [216 * maxSplit][traceEvents]
   int traceEvents = 0;
+  bool traceLight = false;               // MSCCL_AMD_TRACE=2: start / end per workgroup, small kernel kept
   msccl::NpkitLog* dNpkit = nullptr;      // MSCCL_AMD_NPKIT (npkit.cc)
   msccl::NpkitEvent* dNpkitEvents = nullptr;
   uint64_t* dNpkitHeads = nullptr;

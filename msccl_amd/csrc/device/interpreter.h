@@ -1251,6 +1251,7 @@ struct Interp {
   // are run()'s; what goes is the 64-bit iteration arithmetic and most of the scalar state the
   // big loop keeps live (SGPR spills), a few us per launch.
   __device__ __forceinline__ void runSmall(const RankWork& w, int local) {
+    const uint64_t tStart = w.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // MSCCL_AMD_TRACE=2
     redArg = 0;
     trace = nullptr;
     nkBuf = nullptr;
@@ -1326,6 +1327,20 @@ struct Interp {
         if (!runPass(grid, iter)) break;
     }
     epilogue(w, bid, sub, workIndex);
+    if (w.trace != nullptr && tid == 0) {  // light trace: this workgroup's start and end only
+      TraceEvent* tr = w.trace + (size_t)(bid * maxSplit + sub) * w.traceEvents;
+      TraceEvent e;
+      e.ts = __builtin_amdgcn_s_memrealtime();
+      e.type = kEvEnd;
+      e.step = 0;
+      e.arg = 0;
+      tr[1] = e;
+      e.ts = tStart;
+      e.type = kEvHeader;
+      e.step = 2;
+      e.arg = (uint32_t)workIndex;
+      tr[0] = e;
+    }
   }
 };
 

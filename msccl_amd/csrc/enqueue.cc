@@ -275,7 +275,7 @@ bool smallEligible(const Planned& p, const RankWork& w) {
   const int64_t k = cs > 0 ? sp / cs : 0, m = std::min<int64_t>(std::max<int>(1, w.merge), std::max<int64_t>(1, k));
   const bool onePass = sp <= cs || (cs > 0 && sp % cs == 0 && k % m == 0);
   return comm->knobs.smallKernel && p.plan.ringColl == 0 && p.plan.proto == kProtoLL && p.op.devOp <= 3 &&
-         onePass && w.trace == nullptr && w.npkit == nullptr &&
+         onePass && (w.trace == nullptr || comm->traceLight) && w.npkit == nullptr &&
          (w.split & (w.split - 1)) == 0 &&
          p.plan.sizePerChunk * maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop) *
                  refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit element offsets

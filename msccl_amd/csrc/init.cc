@@ -197,6 +197,7 @@ ncclResult_t commFinish(ncclComm* comm) {
   dc.llFlagMask = comm->llFlagMask;
   dc.llCleanMask = comm->llCleanMask;
   if (envInt("MSCCL_AMD_TRACE", 0) > 0) {
+    comm->traceLight = envInt("MSCCL_AMD_TRACE", 0) == 2;
     comm->traceEvents = (int)std::max<int64_t>(8, std::min<int64_t>(65535, envInt("MSCCL_AMD_TRACE_EVENTS", 256)));
     size_t bytes = (size_t)kMaxTb * comm->maxSplit * comm->traceEvents * sizeof(TraceEvent);
     NCCLCHECK(hipErr(hipMalloc(&comm->dTrace, bytes), "hipMalloc trace"));

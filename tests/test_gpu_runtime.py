@@ -213,8 +213,9 @@ def test_c_caller_allreduce(tmp_path):
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("sched", ["allpairs", "pair"])  # pair: the fused exchange (LL)
 @pytest.mark.parametrize("proto", ["LL", "Simple"])
-def test_hip_graph_capture_and_replay(proto, tmp_path):
+def test_hip_graph_capture_and_replay(proto, sched, tmp_path):
     """A grouped AllReduce captured into a hipGraph replays correctly: the launch epoch that
     drives the dependency flags lives on the device (DevComm::epoch), not in the captured
     arguments."""
@@ -222,7 +223,8 @@ def test_hip_graph_capture_and_replay(proto, tmp_path):
     import msccl_amd as M
     from msccl_amd import xmlgen
     xml = tmp_path / "ap.xml"
-    xml.write_text(xmlgen.allreduce_allpairs(2, 2, proto))
+    xml.write_text(xmlgen.allreduce_allpairs(2, 2, proto) if sched == "allpairs" else
+                   xmlgen.allreduce_pair_oneshot(2, proto))
     os.environ["MSCCL_XML_FILES"] = str(xml)
     n, count = 2, 8 * 5000
     comms = M.Comm.init_all([0] * n)

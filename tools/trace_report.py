@@ -14,7 +14,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ["MSCCL_AMD_TRACE"] = "1"
+os.environ.setdefault("MSCCL_AMD_TRACE", "1")  # 2: start / end only, small kernel kept
 import msccl_amd as M  # noqa: E402
 from msccl_amd import xmlgen  # noqa: E402
 
