@@ -440,14 +440,20 @@ def main():
     verified = []
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     # Clock warm-up before the sweep: an idle GPU starts the first timed size at low clocks (the
-    # 128 B point once read 27 us instead of 8-9 us); about 0.3 s of mid-size AllReduces first.
+    # 128 B point once read 27 us instead of 8-9 us).  One process: about 0.3 s of mid-size
+    # AllReduces.  Several: every rank must issue the same number of collectives, so a fixed count.
     wsize = min(maxb, 1 << 20)
     if (wsize // ts) % algos[tier_of(tiers, wsize)[3]]["nchunksperloop"] == 0:
-        t_end = time.perf_counter() + 0.3
-        while time.perf_counter() < t_end:
-            for _ in range(10):
+        if multi:
+            for _ in range(1000):
                 one_step(wsize)
             torch.cuda.synchronize()
+        else:
+            t_end = time.perf_counter() + 0.3
+            while time.perf_counter() < t_end:
+                for _ in range(10):
+                    one_step(wsize)
+                torch.cuda.synchronize()
         barrier()
     for nbytes in sizes:
         cnt = nbytes // ts
