@@ -41,7 +41,10 @@ enum OpType : uint8_t {
   // `s` fused with the `rrc` that follows it (same source chunks, same peer): the device image of
   // a thread block whose exchange both ends run as one pass (transport.cc: fusableTbs); never
   // from XML
-  kSendRecvReduceCopy = 10
+  kSendRecvReduceCopy = 10,
+  // `s` fused with the `cpy` of the same source chunks that follows it: one pass that sends the
+  // source and copies it (the ring's copy-send); never from XML
+  kSendCopy = 11
 };
 
 // Device reduction ops (ncclDevRedOp_t, devcomm.h): Sum, Prod, Max, Min, PreMulSum, SumPostDiv

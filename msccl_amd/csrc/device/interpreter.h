@@ -30,7 +30,8 @@
 namespace msccl {
 
 enum : int { tSend = 0, tRecv = 1, tRCS = 2, tRRS = 3, tRRC = 4, tRRCS = 5, tCpy = 6, tRe = 7, tCopySend = 9,
-             tSendRrc = 10 /* s fused with the rrc after it (transport.cc: fusableTbs) */ };
+             tSendRrc = 10 /* s fused with the rrc after it (transport.cc: fusableTbs) */,
+             tSendCpy = 11 /* s fused with the cpy of the same source after it: a copy-send */ };
 enum : int { pLL = 0, pLL128 = 1, pSimple = 2 };
 
 struct alignas(16) BlockShared {
@@ -133,7 +134,8 @@ struct Interp {
       case tSendRrc: return NPKIT_EVENT_RECV_REDUCE_COPY_ENTRY;
       case tRRCS: return NPKIT_EVENT_RECV_REDUCE_COPY_SEND_ENTRY;
       case tCpy: return NPKIT_EVENT_LOCAL_COPY_ENTRY;
-      case tCopySend: return NPKIT_EVENT_COPY_SEND_ENTRY;
+      case tCopySend:
+      case tSendCpy: return NPKIT_EVENT_COPY_SEND_ENTRY;
       default: return NPKIT_EVENT_REDUCE_ENTRY;
     }
   }
@@ -1145,7 +1147,9 @@ struct Interp {
         DevTransfer t = loadTransfer(&tr[i]);
         const bool fused = fuseable<false>(t);
         if (t.type == tSendRrc && !fused) t.type = tSend;
-        const DevTransfer td = fused ? loadTransfer(&tr[i + 1]) : t;  // the rrc: output buffer
+        const bool sendCpy = t.type == tSendCpy;  // s + cpy as one copy-send (dst: the cpy's)
+        if (sendCpy) t.type = tCopySend;
+        const DevTransfer td = fused || sendCpy ? loadTransfer(&tr[i + 1]) : t;  // output buffer
         if (t.numDeps > 0) {
           nk(NPKIT_EVENT_DEP_CHECK_ENTRY, t.numDeps);
           waitDeps(t, flags, workIndex, iter, sub, maxSplit);
@@ -1218,7 +1222,7 @@ struct Interp {
           ev(kEvPrimEnd, (uint16_t)i, 0);
         }
         if (stop) break;
-        if (fused) {  // the s published nothing (fusableTbs); the rrc's flag below
+        if (fused || sendCpy) {  // the s published nothing (transport.cc); the second transfer's flag below
           step++;
           i++;
           t = td;
@@ -1278,7 +1282,9 @@ struct Interp {
         DevTransfer t = loadTransfer(&tr[i]);
         const bool fused = fuseable<true>(t);
         if (t.type == tSendRrc && !fused) t.type = tSend;
-        const DevTransfer td = fused ? loadTransfer(&tr[i + 1]) : t;
+        const bool sendCpy = t.type == tSendCpy;
+        if (sendCpy) t.type = tCopySend;
+        const DevTransfer td = fused || sendCpy ? loadTransfer(&tr[i + 1]) : t;
         if (t.numDeps > 0) {
           waitDeps(t, w.flags, workIndex, iter, sub, maxSplit);
           step += t.numDeps - 1;
@@ -1310,7 +1316,7 @@ struct Interp {
             return false;
           if (t.type == tRe && c == 0) step += t.numReds - 1;
         }
-        if (fused) {
+        if (fused || sendCpy) {
           step++;
           i++;
           t = td;

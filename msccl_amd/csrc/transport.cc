@@ -478,6 +478,13 @@ ncclResult_t algoUpload(ncclComm* comm) {
       if (g < comm->algoFuse.size())
         for (const FuseCandidate& f : comm->algoFuse[g])
           if (f.tb == b) ts[f.index].type = kSendRecvReduceCopy;
+      // s followed by a cpy of the same source chunks (an out-of-place AllGather's own block):
+      // one copy-send pass reads the source once.  A local change: the FIFO steps are the s's.
+      for (size_t i = 0; comm->knobs.fuse && i + 1 < ts.size(); i++)
+        if (ts[i].type == kSend && ts[i + 1].type == kLocalCopy && ts[i].srcbuf == ts[i + 1].srcbuf &&
+            ts[i].srcoff == ts[i + 1].srcoff && ts[i].count == ts[i + 1].count && ts[i].hasDep == 0 &&
+            ts[i + 1].numDeps == 0)
+          ts[i].type = kSendCopy;
       putImage(img, (size_t)b * stride, h, ts, tb.depBid, tb.depStep, tb.redSrcOff);
     }
     NCCLCHECK(uploadImages(img, &d));

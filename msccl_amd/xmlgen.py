@@ -362,17 +362,15 @@ def allgather_allpairs(n: int, instances: int = 1, proto: str = "Simple", inplac
         peers = [p for p in range(n) if p != r]
         tbs = []
         tid = 0
-        if not inplace:
-            for k in range(I):
-                tb = _Tb(tid, -1, -1, k)
-                tb.add("cpy", "i", k, "o", r * I + k, 1)
-                tbs.append(tb)
-                tid += 1
-        for p in peers:
+        # out of place: the own block's copy follows the first peer's send of the same chunk, so
+        # the interpreter runs the two as one copy-send (transport.cc: kSendCopy)
+        for pi, p in enumerate(peers):
             for k in range(I):
                 tb = _Tb(tid, p, p, k)
                 tid += 1
                 tb.add("s", "i", k, "o", r * I + k, 1)
+                if not inplace and pi == 0:
+                    tb.add("cpy", "i", k, "o", r * I + k, 1)
                 tb.add("r", "i", k, "o", p * I + k, 1)
                 tbs.append(tb)
         gpus[r] = (I, ncpl, 0, tbs)

@@ -170,3 +170,18 @@ def test_fusable_image_on_other_protocols(proto, count, dt, tmp_path):
         assert all(len(c.info()["algoFuse"][0]) > 0 for c in cr.comms)
     got, want, _ = run_collective(xml, 2, L.ALLREDUCE, count, dt, 0, True, seed=12, tmpdir=str(tmp_path))
     _check(got, want, proto)
+
+
+@pytest.mark.parametrize("n,proto,count,dt", [(2, "Simple", 1 << 20, 7), (2, "LL", 3000, 6), (4, "Simple", 12345, 9),
+                                              (8, "LL", 1 << 16, 7), (2, "LL128", 1 << 18, 2)])
+def test_allgather_send_copy_fused(n, proto, count, dt, tmp_path, monkeypatch):
+    """Out-of-place AllGather: the own block's cpy follows the first peer's s of the same chunk and
+    the two run as one copy-send (transport.cc: kSendCopy); same bytes as unfused, oracle values."""
+    xml = xmlgen.allgather_allpairs(n, 2, proto, inplace=False)
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MSCCL_AMD_FUSE", fuse)
+        got, want, _ = run_collective(xml, n, L.ALLGATHER, count, dt, 0, False, seed=21, tmpdir=str(tmp_path))
+        _check(got, want, "AllGather fuse=%s" % fuse)
+        res[fuse] = got
+    _check(res["1"], res["0"], "AllGather fused vs unfused")
