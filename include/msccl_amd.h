@@ -19,6 +19,12 @@ extern "C" {
  * resulting program as JSON into out[0..outLen).  Returns the ncclResult_t of the load. */
 int mscclAmdAlgoJson(const char* xmlPath, int rank, int nranks, char* out, size_t outLen);
 
+/* The thread blocks of that program whose first FIFO transfers are an `s` then an `rrc` of the same
+ * source chunks with one peer: the exchanges this rank offers to run fused (init fuses one only
+ * when the peer's thread block on the connection offers it too).  JSON {"fusable":[[tb, index,
+ * channel, peer], ...]}.  No GPU needed. */
+int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, size_t outLen);
+
 /* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the launch plan
  * (enqueue.cc:591-734).  coll uses ncclFunc_t numbering (AllGather=2, ReduceScatter=3,
  * AllReduce=4).  Writes JSON {"algo":i,...} or {"algo":-1}.  No GPU needed. */

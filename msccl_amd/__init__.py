@@ -84,6 +84,7 @@ def lib() -> ctypes.CDLL:
     L.ncclGroupStart.argtypes = []
     L.ncclGroupEnd.argtypes = []
     L.mscclAmdAlgoJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
+    L.mscclAmdFusableJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
     L.mscclAmdPlanJson.argtypes = [ctypes.c_char_p, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
     L.mscclAmdCommInfo.argtypes = [vp, ctypes.c_char_p, sz]
     L.mscclAmdNpkitDump.argtypes = [vp, ctypes.c_char_p]
@@ -132,6 +133,14 @@ def algo_json(xml_path: str, rank: int, nranks: int) -> dict:
     buf = ctypes.create_string_buffer(1 << 24)
     _check(lib().mscclAmdAlgoJson(xml_path.encode(), rank, nranks, buf, len(buf)), "mscclAmdAlgoJson")
     return json.loads(buf.value.decode())
+
+
+def fusable_json(xml_path: str, rank: int, nranks: int) -> list:
+    """The exchanges one rank of a schedule offers to run fused (transport.cc: fusableTbs):
+    [[tb, index of its s, channel, peer], ...]."""
+    buf = ctypes.create_string_buffer(1 << 20)
+    _check(lib().mscclAmdFusableJson(xml_path.encode(), rank, nranks, buf, len(buf)), "mscclAmdFusableJson")
+    return json.loads(buf.value.decode())["fusable"]
 
 
 def try_algo_json(xml_path: str, rank: int, nranks: int):

@@ -31,6 +31,19 @@ int mscclAmdAlgoJson(const char* xmlPath, int rank, int nranks, char* out, size_
   return putOut(algoToJson(a), out, outLen);
 }
 
+int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, size_t outLen) {
+  Algorithm a;
+  int r = loadAlgoFromXml(xmlPath, &a, kMaxChannels, rank, nranks);
+  if (r != 0) return r;
+  std::ostringstream o;
+  o << "{\"fusable\":[";
+  const std::vector<FuseCandidate> fc = fusableTbs(a);
+  for (size_t i = 0; i < fc.size(); i++)
+    o << (i ? "," : "") << "[" << fc[i].tb << "," << fc[i].index << "," << fc[i].chan << "," << fc[i].peer << "]";
+  o << "]}";
+  return putOut(o.str(), out, outLen);
+}
+
 int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_t count, int dtype, int redop,
                      int inPlace, char* out, size_t outLen) {
   std::vector<Algorithm> algos;
