@@ -35,9 +35,11 @@ XGMI_LINK_GBS = 153.0          # task statement, per link (see DESIGN.md calibra
 SIZES = [128 << k for k in range(19)]  # 128 B .. 32 MiB
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs, one rank each (default 1: config C2 with 2 ranks co-resident on cuda:0). "
+                         "Without torch.distributed.run's WORLD_SIZE, N > 1 starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--vranks", type=int, default=2, help="co-resident ranks at --gpus 1 (config C2: 2)")
@@ -53,8 +55,54 @@ def parse():
     ap.add_argument("--extras", default=None,
                     help="also measure C4 (ring Simple bf16 256 MiB) / C5 (RS+AG fp32 64 MiB), e.g. C4,C5 "
                          "(default: both when 8 ranks run one per GPU)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary schedule lines (msccl-tools two-phase all-pairs, RCCL 8n-32tb)")
+    ap.add_argument("--pmc", default="auto", choices=("auto", "off"),
+                    help="auto: at N=1 measure the headline launch's HBM traffic with two rocprofv3 PMC "
+                         "passes (FETCH_SIZE, WRITE_SIZE) of a headline-only child run")
     ap.add_argument("--quiet", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_plan(gpus, env, device_count):
+    """How `bench.py --gpus N` runs (the reference's harness is `mpirun -np 8 ... all_reduce_perf
+    -g 1`, README.md:57: one process per GPU).  Returns (mode, detail):
+      ("rank", W)     started by torch.distributed.run (WORLD_SIZE = W > 1): this process is one rank
+      ("local", 1)    N = 1: config C2, its 2 ranks co-resident on cuda:0, one process
+      ("spawn", N)    N > 1 without WORLD_SIZE: start N rank processes (torch.distributed.run),
+                      relay rank 0's line; this process never touches the GPU
+      ("refuse", msg) fewer GPUs than ranks (MSCCL_AMD_BENCH_ONE_GPU=1 rehearses N processes on
+                      cuda:0 instead), or --gpus disagreeing with WORLD_SIZE
+    `device_count` is torch.cuda.device_count(), which does not initialise the GPU."""
+    one_gpu = env.get("MSCCL_AMD_BENCH_ONE_GPU") == "1"
+    world = int(env.get("WORLD_SIZE", "1") or "1")
+    if world > 1:
+        if gpus is not None and gpus != world:
+            return "refuse", "--gpus %d but WORLD_SIZE=%d" % (gpus, world)
+        if device_count < world and not one_gpu:
+            return "refuse", ("%d ranks need %d GPUs, %d visible (MSCCL_AMD_BENCH_ONE_GPU=1 rehearses them "
+                              "on one GPU)" % (world, world, device_count))
+        return "rank", world
+    n = gpus or 1
+    if n <= 1:
+        return "local", 1
+    if device_count < n and not one_gpu:
+        return "refuse", ("--gpus %d needs %d GPUs, %d visible (MSCCL_AMD_BENCH_ONE_GPU=1 rehearses %d "
+                          "processes on one GPU)" % (n, n, device_count, n))
+    return "spawn", n
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start n rank processes with torch.distributed.run on 127.0.0.1 and wait for them; their
+    stdout (rank 0's JSON line) is this process's.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    return subprocess.call(cmd)
 
 
 def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only: bool = False, fused=()):
@@ -174,17 +222,26 @@ def cpu_baseline(n: int, nbytes: int, dt: int, seconds: float):
             "ms_per_allreduce": round(t * 1e3, 4)}
 
 
-def workload_desc(multi: bool, n: int, proto: str, dtname: str) -> str:
+def workload_desc(multi: bool, n: int, proto: str, dtname: str, one_gpu: bool = False) -> str:
     if not multi:
         return ("C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
                 "(fused launch, local HBM in place of xGMI)" % (n, proto, dtname))
+    if one_gpu:
+        return ("rehearsal: %d rank processes sharing one MI355X (hipIpc FIFOs, local HBM in place of "
+                "xGMI), all-pairs %s AllReduce, %s" % (n, proto, dtname))
     return ("%s: %d-rank all-pairs %s AllReduce over xGMI, %s, one rank per GPU"
             % ("C3" if n == 8 else "C2-family", n, proto, dtname))
 
 
-def pmc_traffic(cfg_key: dict):
+TIER_KINDS = {"a": "allreduce_allpairs (two-phase: s, r, re, s, r; msccl-tools form)",
+              "o": "allreduce_oneshot", "O": "allreduce_oneshot (rank-ordered)",
+              "p": "allreduce_pair_oneshot (s, rrc per thread block)", "r": "allreduce_ring"}
+
+
+def pmc_traffic(cfg_key: dict, src_hash: str):
     """HBM bytes per headline launch from the committed rocprofv3 PMC summary of the same
-    configuration (tools/profile.sh -> profiles/<tag>_pmc.json), or (None, None)."""
+    configuration (tools/profile.sh -> profiles/<tag>_pmc.json) taken on the same device sources
+    (its "kernel_src" stamp equals kernel_src_hash()), or (None, None)."""
     import glob
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")), reverse=True):
         try:
@@ -193,6 +250,8 @@ def pmc_traffic(cfg_key: dict):
         except (OSError, ValueError):
             continue
         c = bench.get("config", {})
+        if pmc.get("kernel_src") != src_hash:
+            continue
         if all(c.get(k, {} if k == "knobs" else None) == v for k, v in cfg_key.items()) and pmc.get("traffic_bytes_per_launch"):
             return round(pmc["traffic_bytes_per_launch"]), os.path.relpath(f, ROOT)
     return None, None
@@ -348,18 +407,180 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
             c.destroy()
 
 
+RCCL_32TB = "/opt/rocm/share/rccl/msccl-algorithms/allreduce-allpairs-8n-ll-32tb.xml"
+
+
+def secondary_schedules(multi: bool, n: int, nbytes: int):
+    """The north star's number is "for the all-pairs XML schedule": next to the headline tier, the
+    same AllReduce through (1) the msccl-tools two-phase all-pairs form (xmlgen.allreduce_allpairs,
+    the shape of the RCCL-shipped allreduce-allpairs-8n XMLs) at the headline's ranks and size, and
+    (2) at N=1 the RCCL-shipped 8n-32tb LL schedule itself on 8 co-resident ranks, fp16 (config C3's
+    shape; maxBytes raised from 64 KiB so it admits 32 MiB, as tests/test_gpu_configs.py does).
+    Returns [(name, xml_text, ranks, bytes, dtype)]."""
+    out = [("allpairs_two_phase", xmlgen.allreduce_allpairs(n, 16 if n <= 2 else 4, "LL", True, 0, 1 << 40,
+                                                             name="sec_allpairs"), n, nbytes, None)]
+    if not multi and os.path.exists(RCCL_32TB):
+        x = open(RCCL_32TB).read().replace('maxBytes="65536"', 'maxBytes="%d"' % ((32 << 20) + 1))
+        out.append(("rccl_allpairs_8n_ll_32tb", x, 8, 32 << 20, M.FLOAT16))
+    return out
+
+
+def run_secondary(name: str, xml_text: str, n: int, nbytes: int, dt: int, a, multi: bool, rank: int,
+                  tmp: str) -> dict:
+    """One schedule, one size: warmup, K timed AllReduces (HIP events on the collective's stream
+    and the host clock, max over ranks), then one step on exact integers that must equal the exact
+    sum.  Co-resident ranks at N=1 (n of them on cuda:0), one rank per process otherwise."""
+    import torch
+    pth = os.path.join(tmp, "bench_sec_%s_%d.xml" % (name, os.getpid()))
+    with open(pth, "w") as f:
+        f.write(xml_text)
+    os.environ["MSCCL_XML_FILES"] = pth
+    dev = torch.device("cuda", torch.cuda.current_device())
+    comms = init_comms(multi, n if multi else 1, rank, n)
+    try:
+        ts = M.TYPE_SIZE[dt]
+        cnt = nbytes // ts
+        tdt = {M.FLOAT32: torch.float32, M.FLOAT16: torch.float16, M.BFLOAT16: torch.bfloat16}[dt]
+        ranks = [rank] if multi else list(range(n))
+        bufs = [torch.empty(cnt, dtype=tdt, device=dev).uniform_(-1, 1) for _ in ranks]
+        stream = torch.cuda.Stream(dev)
+        stream.wait_stream(torch.cuda.current_stream(dev))
+
+        def step():
+            with M.group():
+                for c, b in zip(comms, bufs):
+                    c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+        for _ in range(max(1, a.warmup)):
+            step()
+        k = max(1, a.steps)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if multi:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(k):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if multi:
+            torch.distributed.barrier()
+        t = (time.perf_counter() - t0) / k
+        ev_ms = ev0.elapsed_time(ev1) / k
+        if multi:
+            tt = torch.tensor([t, ev_ms], dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            t, ev_ms = float(tt[0]), float(tt[1])
+        if any(c.async_error() != 0 for c in comms):
+            raise RuntimeError("kernel reported an error (timeout/abort)")
+        small = comms[0].info()["last"].get("small", 0) == 1
+        j = torch.arange(cnt, device=dev, dtype=torch.int64)
+        pat = [((j * 7 + r * 3 + (j >> 5)) % 9 - 4).to(torch.float32) for r in range(n)]
+        for r, b in zip(ranks, bufs):
+            b.copy_(pat[r].to(tdt))
+        want = sum(pat).to(tdt)
+        torch.cuda.synchronize()
+        step()
+        torch.cuda.synchronize()
+        good = all(torch.equal(b, want) for b in bufs)
+        if multi:
+            g = torch.tensor([1 if good else 0], dtype=torch.int32)
+            torch.distributed.all_reduce(g, op=torch.distributed.ReduceOp.MIN)
+            good = bool(g.item())
+        return {"ranks": n, "bytes": nbytes, "dtype": {M.FLOAT32: "f32", M.FLOAT16: "f16", M.BFLOAT16: "bf16"}[dt],
+                "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
+                "busbw": round(nbytes / t * 2 * (n - 1) / n / 1e9, 3), "verified": good, "steps": k,
+                "kernel": "mscclSmallKernel" if small else "mscclKernel"}
+    finally:
+        for c in comms:
+            c.destroy()
+
+
+def kernel_src_hash() -> str:
+    """Hash of the device sources: a PMC profile is evidence for the current kernel only if it was
+    taken on the same sources (tools/parse_prof.py stamps it)."""
+    import hashlib
+    h = hashlib.sha1()
+    d = os.path.join(ROOT, "msccl_amd", "csrc", "device")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".h", ".hip")):
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(f.encode() + fh.read())
+    return h.hexdigest()[:12]
+
+
+def live_pmc(a, timeout_s: int = 150):
+    """HBM traffic of the headline launch, measured in this run: two rocprofv3 PMC passes
+    (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass on gfx950) over a child bench run of
+    the headline size only, so every interpreter dispatch in it is a headline launch.  Per the
+    MI355X guide's HBM section: traffic = (2 x FETCH_SIZE + WRITE_SIZE) x 1 KiB (gfx950 FETCH_SIZE
+    reports half of a 16-B-per-lane streaming read).  Returns (bytes per launch, detail) or (None, why)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not found"
+    child = [sys.executable, os.path.abspath(__file__), "--sizes", "33554432", "--steps", "10", "--warmup", "3",
+             "--no-cpu", "--quiet", "--no-secondary", "--pmc", "off", "--extras", "",
+             "--vranks", str(a.vranks), "--proto", a.proto]
+    if a.dtype:
+        child += ["--dtype", a.dtype]
+    if a.instances:
+        child += ["--instances", str(a.instances)]
+    if a.tiers:
+        child += ["--tiers", a.tiers]
+    vals = {}
+    tmp = tempfile.mkdtemp(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", counter, "--output-format", "csv",
+                   "-d", d, "-o", "run", "--"] + child
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=timeout_s + 30)
+            if r.returncode != 0:
+                return None, "rocprofv3 --pmc %s exited %d: %s" % (counter, r.returncode,
+                                                                   r.stderr.decode(errors="replace")[-200:])
+            v = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                with open(f, newline="") as fh:
+                    for row in csv.DictReader(fh):
+                        if "msccl" in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                            v.append(float(row["Counter_Value"]))
+            if not v:
+                return None, "no %s rows for the interpreter kernel" % counter
+            vals[counter] = (sum(v) / len(v), len(v))
+    except (OSError, subprocess.SubprocessError) as e:
+        return None, "rocprofv3 pass failed: %s" % e
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    fetch, nf = vals["FETCH_SIZE"]
+    write, nw = vals["WRITE_SIZE"]
+    return (2.0 * fetch + write) * 1024.0, {"fetch_size_kib": round(fetch, 1), "write_size_kib": round(write, 1),
+                                           "launches": [nf, nw]}
+
+
 def main():
     a = parse()
+    import torch
+    mode, detail = launch_plan(a.gpus, os.environ, torch.cuda.device_count())
+    if mode == "refuse":
+        print("bench.py: %s" % detail, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(detail, sys.argv[1:]))
     # Only the result line goes to stdout: libraries that print there (gloo's connection report,
     # HIP runtime messages) are sent to stderr at the file-descriptor level.
     sys.stdout.flush()
     result_fd = os.dup(1)
     os.dup2(2, 1)
-    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    multi = world > 1
+    multi = mode == "rank"
+    one_gpu = os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") == "1"
     n = world if multi else a.vranks
     dtname = a.dtype or ("fp16" if (multi and world >= 8) else "fp32")
     dt = M.DTYPE_NAMES[dtname]
@@ -376,7 +597,7 @@ def main():
         import torch.distributed as dist
         # MSCCL_AMD_BENCH_ONE_GPU=1 puts every rank on cuda:0: rehearses the multi-process path
         # (bootstrap, hipIpc FIFOs, barriers, max over ranks) on a one-GPU box
-        local = 0 if os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") == "1" else local
+        local = 0 if one_gpu else local
         torch.cuda.set_device(local)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         devs = [torch.device("cuda", local)]
@@ -393,7 +614,7 @@ def main():
     xgmi_cal = None
     if multi:
         # SURVEY 8(d) calibration: one-way peer copy cuda:0 -> cuda:1 (xGMI), 256 MiB, rank 0
-        if rank == 0 and torch.cuda.device_count() > 1 and os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") != "1":
+        if rank == 0 and torch.cuda.device_count() > 1 and not one_gpu:
             xgmi_cal = calibrate_xgmi()
         barrier()
     stream = torch.cuda.Stream(devs[0])
@@ -442,8 +663,10 @@ def main():
     # Clock warm-up before the sweep: an idle GPU starts the first timed size at low clocks (the
     # 128 B point once read 27 us instead of 8-9 us).  One process: about 0.3 s of mid-size
     # AllReduces.  Several: every rank must issue the same number of collectives, so a fixed count.
+    # (A one-size run, e.g. a rocprofv3 pass over the headline, skips it: its warmup steps warm the
+    # clocks, and every interpreter dispatch of the run is then a launch of that size.)
     wsize = min(maxb, 1 << 20)
-    if (wsize // ts) % algos[tier_of(tiers, wsize)[3]]["nchunksperloop"] == 0:
+    if len(sizes) > 1 and (wsize // ts) % algos[tier_of(tiers, wsize)[3]]["nchunksperloop"] == 0:
         if multi:
             for _ in range(1000):
                 one_step(wsize)
@@ -498,19 +721,24 @@ def main():
         bus = algbw * 2 * (n - 1) / n
         algo = algos[tier[3]]
         size_per = cnt // ncpl
-        hbm, wire = schedule_bytes(algo, size_per, ts, proto_id, fused=fused.get(tier[3], ()))
-        payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True, fused=fused.get(tier[3], ()))
+        # the fused s + rrc pass runs only in mscclSmallKernel: the discount of one source read
+        # applies to sizes whose launches ran there (comm info "last": the kernel of the last launch)
+        small = comms[0].info()["last"].get("small", 0) == 1
+        fz = fused.get(tier[3], ()) if small else ()
+        hbm, wire = schedule_bytes(algo, size_per, ts, proto_id, fused=fz)
+        payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True, fused=fz)
         ok = verify(nbytes)
         verified.append(ok)
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
-                        "payload_bytes_per_rank": payload, "verified": ok,
+                        "payload_bytes_per_rank": payload, "verified": ok, "small": small,
+                        "fused": bool(fz), "tier": tier[4],
                          "algbw": round(algbw, 3), "busbw": round(bus, 3),
                          "hbm_bytes_per_rank": hbm, "wire_bytes_per_rank": wire})
         if not a.quiet and rank == 0:
             print("# %10d B  %9.2f us  algbw %8.2f  busbw %8.2f GB/s" % (nbytes, t * 1e6, algbw, bus),
                   file=sys.stderr, flush=True)
     head = results[-1]
-    headline_small = comms[0].info()["last"].get("small", 0) == 1  # which kernel the headline ran
+    headline_small = head["small"]  # which kernel the headline ran
     # roofline of the dominant (largest) launch
     ranks_on_gpu = 1 if multi else n
     kernel_s = head["kernel_ms"] / 1e3
@@ -531,16 +759,42 @@ def main():
         roof["xgmi"] = {"busbw": head["busbw"], "peak": link, "frac": round(head["busbw"] / link, 4),
                         "ll_ceiling": round(link * {0: 0.5, 1: 0.75}.get(proto_id, 1.0), 1),
                         "link_gbs_assumed": XGMI_LINK_GBS, "link_gbs_measured": xgmi_cal}
-    workload = workload_desc(multi, n, a.proto, dtname)
+    workload = workload_desc(multi, n, a.proto, dtname, one_gpu)
     knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("MSCCL_AMD_") and k != "MSCCL_AMD_TIMEOUT_SEC"}
     cfg_key = {"workload": workload, "bytes_per_rank": head["bytes"], "instances_large": inst, "knobs": knobs}
-    roof["traffic"], roof["traffic_source"] = pmc_traffic(cfg_key)
+    schedule = TIER_KINDS[head["tier"]] + (", s + rrc fused into one pass" if head["fused"] else "")
     e2e = None
     if a.e2e and rank == 0 and not multi:
         e2e = measure_e2e(comms, n, maxb, dt, ts, stream, devs[0])
     for c in comms:
         c.destroy()
     comms = []
+    secondary = {}
+    if not a.no_secondary and head["bytes"] == 32 << 20:
+        for name, x, sn, sb, sdt in secondary_schedules(multi, n, head["bytes"]):
+            try:
+                secondary[name] = run_secondary(name, x, sn, sb, sdt if sdt is not None else dt, a, multi, rank, tmp)
+            except Exception as e:  # noqa: BLE001  (reported in the JSON line, the headline stands)
+                secondary[name] = {"error": str(e)[:300]}
+            if rank == 0 and not a.quiet:
+                print("# secondary %s: %s" % (name, secondary[name]), file=sys.stderr, flush=True)
+    # HBM traffic of the headline launch: measured now (N=1, rocprofv3 on PATH), else the committed
+    # profile of the same configuration, valid only if taken on the same device sources
+    src_hash = kernel_src_hash()
+    if a.pmc == "auto" and not multi and rank == 0:
+        tb, detail = live_pmc(a)
+        if tb is not None:
+            roof["traffic"] = round(tb)
+            roof["traffic_source"] = {"measured": "this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over "
+                                                  "a headline-only child run", **detail, "kernel_src": src_hash}
+        else:
+            roof["traffic_source"] = {"measured": None, "why": detail}
+    if roof["traffic"] is None:
+        tb, src = pmc_traffic(cfg_key, src_hash)
+        if tb is not None:
+            roof["traffic"], roof["traffic_source"] = tb, {"profile": src, "kernel_src": src_hash}
+    if roof["traffic"] is not None:
+        roof["traffic_over_algorithmic"] = round(roof["traffic"] / roof["algorithmic_bytes_per_launch"], 4)
     extras = {}
     which = a.extras if a.extras is not None else ("C4,C5" if multi and world == 8 else "")
     for cfg in [w for w in which.split(",") if w]:
@@ -558,7 +812,8 @@ def main():
         "vs_baseline": None, "dtype": {"fp32": "f32", "fp16": "f16", "bf16": "bf16"}.get(dtname, dtname),
         "data": "synthetic",
         "config": {"workload": workload,
-                   "ranks": n, "bytes_per_rank": head["bytes"], "schedule": "allreduce_allpairs",
+                   "ranks": n, "devices": 1 if (one_gpu or not multi) else world,
+                   "bytes_per_rank": head["bytes"], "schedule": schedule,
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
                    "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot", "O": "oneshot-ordered",
                                                  "p": "pair-oneshot", "r": "ring"}[t[4]]] for t in tiers],
@@ -574,10 +829,12 @@ def main():
                       "algbw_sum_gbs": round(head["bytes"] / (head["ms"] / 1e3) / 1e9 * n, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw", "verified")} for r in results],
+        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw", "verified", "small")} for r in results],
     }
     if e2e:
         out["e2e"] = e2e
+    if secondary:
+        out["schedules"] = secondary
     if extras:
         out["configs"] = extras
     if rank == 0:

@@ -52,6 +52,15 @@ int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex);
  * geometry.  Synchronises the device.  ncclInvalidUsage when tracing is off. */
 int mscclAmdTraceRead(ncclComm_t comm, void* out, size_t outBytes, int* slots, int* events);
 
+/* 16-B line atomicity probe: the gate for LL128 towards another GPU (the
+ * reference enables LL128 only where line atomicity holds, tuning.cc:210-214).  Writers on
+ * `writerDev` store nLines 16-B lines {payload(k), payload(k), payload(k), k} for k = 1..iters
+ * into uncached memory of `readerDev` (the FIFO memory) while readers there poll them with 16-B
+ * loads for at most `seconds`.  out[0] = lines observed with a flag, out[1] = observed lines whose
+ * payload does not match their flag (torn), out[2] = lines that reached k = iters. */
+int mscclAmdLineTearProbe(int writerDev, int readerDev, int nLines, int iters, double seconds,
+                          unsigned long long* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -91,6 +91,7 @@ def lib() -> ctypes.CDLL:
     L.mscclAmdBootstrapAllgather.argtypes = [ctypes.POINTER(UniqueId), i, i, vp, sz, vp]
     L.mscclAmdAlgoBlocks.argtypes = [vp, i]
     L.mscclAmdTraceRead.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
+    L.mscclAmdLineTearProbe.argtypes = [i, i, i, i, ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
     _lib = L
     return L
 
@@ -135,12 +136,22 @@ def algo_json(xml_path: str, rank: int, nranks: int) -> dict:
     return json.loads(buf.value.decode())
 
 
-def fusable_json(xml_path: str, rank: int, nranks: int) -> list:
+def fusable_json(xml_path: str, rank: int, nranks: int, key: str = "fusable") -> list:
     """The exchanges one rank of a schedule offers to run fused (transport.cc: fusableTbs):
-    [[tb, index of its s, channel, peer], ...]."""
+    [[tb, index of its s, channel, peer], ...]; key "sendcopy": the s + cpy pairs it runs as one
+    copy-send pass (transport.cc: sendCopyFusable), [[tb, index of the s], ...]."""
     buf = ctypes.create_string_buffer(1 << 20)
     _check(lib().mscclAmdFusableJson(xml_path.encode(), rank, nranks, buf, len(buf)), "mscclAmdFusableJson")
-    return json.loads(buf.value.decode())["fusable"]
+    return json.loads(buf.value.decode())[key]
+
+
+def line_tear_probe(writer_dev: int, reader_dev: int, lines: int = 1 << 16, iters: int = 2000,
+                    seconds: float = 5.0) -> dict:
+    """mscclAmdLineTearProbe (include/msccl_amd.h): 16-B lines written from one device into another
+    device's uncached memory while that device polls them; counts lines seen torn."""
+    out = (ctypes.c_ulonglong * 3)()
+    _check(lib().mscclAmdLineTearProbe(writer_dev, reader_dev, lines, iters, seconds, out), "mscclAmdLineTearProbe")
+    return {"seen": out[0], "torn": out[1], "done": out[2], "lines": lines, "iters": iters}
 
 
 def try_algo_json(xml_path: str, rank: int, nranks: int):

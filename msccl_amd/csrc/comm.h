@@ -162,6 +162,7 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
 ncclResult_t algoUpload(ncclComm* comm);
 int algoSendRunOf(const Algorithm& a);
 std::vector<FuseCandidate> fusableTbs(const Algorithm& a);
+bool sendCopyFusable(const Algorithm& a, const std::vector<Transfer>& ts, size_t i);
 ncclResult_t ringUpload(ncclComm* comm);
 
 // enqueue.cc

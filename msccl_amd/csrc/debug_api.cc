@@ -2,6 +2,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <sstream>
 
 #include <hip/hip_runtime.h>
@@ -40,6 +41,14 @@ int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, si
   const std::vector<FuseCandidate> fc = fusableTbs(a);
   for (size_t i = 0; i < fc.size(); i++)
     o << (i ? "," : "") << "[" << fc[i].tb << "," << fc[i].index << "," << fc[i].chan << "," << fc[i].peer << "]";
+  o << "],\"sendcopy\":[";
+  bool first = true;
+  for (int b = 0; b < a.nBlocks; b++)
+    for (size_t i = 0; i + 1 < a.tbs[b].transfers.size(); i++)
+      if (sendCopyFusable(a, a.tbs[b].transfers, i)) {
+        o << (first ? "" : ",") << "[" << b << "," << i << "]";
+        first = false;
+      }
   o << "]}";
   return putOut(o.str(), out, outLen);
 }
@@ -147,6 +156,58 @@ int mscclAmdTraceRead(ncclComm_t comm, void* out, size_t outBytes, int* slots, i
       hipMemcpy(out, comm->dTrace, bytes, hipMemcpyDeviceToHost) != hipSuccess)
     return ncclUnhandledCudaError;
   return ncclSuccess;
+}
+
+int mscclAmdLineTearProbe(int writerDev, int readerDev, int nLines, int iters, double seconds,
+                          unsigned long long* out) {
+  if (!out || nLines <= 0 || iters <= 0 || seconds <= 0) return ncclInvalidArgument;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess) return ncclUnhandledCudaError;
+  if (writerDev < 0 || readerDev < 0 || writerDev >= ndev || readerDev >= ndev) return ncclInvalidArgument;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  void* lines = nullptr;
+  unsigned long long* cnt = nullptr;
+  hipStream_t rs = nullptr, ws = nullptr;
+  ncclResult_t res = ncclUnhandledCudaError;
+  const size_t bytes = (size_t)nLines * 16;
+  do {
+    // the receiving device owns the lines, in the uncached memory the FIFOs use (transport.cc)
+    if (hipSetDevice(readerDev) != hipSuccess) break;
+    if (hipExtMallocWithFlags(&lines, bytes, hipDeviceMallocUncached) != hipSuccess) break;
+    if (hipMalloc((void**)&cnt, 3 * sizeof(unsigned long long)) != hipSuccess) break;
+    if (hipMemset(lines, 0, bytes) != hipSuccess || hipMemset(cnt, 0, 3 * sizeof(unsigned long long)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess)
+      break;
+    if (hipStreamCreateWithFlags(&rs, hipStreamNonBlocking) != hipSuccess) break;
+    if (hipSetDevice(writerDev) != hipSuccess) break;
+    if (writerDev != readerDev) {
+      hipError_t e = hipDeviceEnablePeerAccess(readerDev, 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) break;
+      (void)hipGetLastError();
+    }
+    if (hipStreamCreateWithFlags(&ws, hipStreamNonBlocking) != hipSuccess) break;
+    // readers first (they bound themselves by time), then the writers
+    if (hipSetDevice(readerDev) != hipSuccess) break;
+    const int rblocks = std::min(1024, (nLines + 255) / 256);
+    if (launchLineReader(lines, nLines, iters, (uint64_t)(seconds * 1e8), cnt, rblocks, rs) != 0) break;
+    if (hipSetDevice(writerDev) != hipSuccess) break;
+    if (launchLineWriter(lines, nLines, iters, std::min(1024, (nLines + 255) / 256), ws) != 0) break;
+    if (hipStreamSynchronize(ws) != hipSuccess) break;
+    if (hipSetDevice(readerDev) != hipSuccess || hipStreamSynchronize(rs) != hipSuccess) break;
+    if (hipMemcpy(out, cnt, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) break;
+    res = ncclSuccess;
+  } while (false);
+  if (ws) {
+    (void)hipSetDevice(writerDev);
+    (void)hipStreamDestroy(ws);
+  }
+  (void)hipSetDevice(readerDev);
+  if (rs) (void)hipStreamDestroy(rs);
+  if (lines) (void)hipFree(lines);
+  if (cnt) (void)hipFree(cnt);
+  (void)hipSetDevice(prev);
+  return res;
 }
 
 }  // extern "C"

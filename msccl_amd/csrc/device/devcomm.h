@@ -15,6 +15,7 @@
 //     produced are the same as with one workgroup (the split is by element, every element
 //     keeps its operations and their order).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
 
@@ -59,10 +60,16 @@ struct NpkitEvent {
 struct NpkitLog {
   NpkitEvent* events;    // [kNpkitDevBuffers][cap]
   uint64_t* heads;       // [kNpkitDevBuffers] events written so far (may exceed cap: the rest dropped)
-  int64_t cpuOffsetNs;   // host system_clock ns = GPU clock ticks * nsPerTick + cpuOffsetNs
+  int64_t cpuOffsetNs;   // host system_clock ns = npkitTicksToNs(GPU clock ticks, clockKHz) + cpuOffsetNs
   int32_t cap;
-  int32_t nsPerTick;     // s_memrealtime period (10 ns at 100 MHz)
+  int32_t clockKHz;      // s_memrealtime rate (100000 kHz on MI355X)
 };
+// GPU clock ticks -> ns for a clock of khz kHz, exact for any rate (no rounded period: a 3.33-ns
+// period taken as 3 ns would drift linearly) and free of overflow for any uptime.
+__host__ __device__ inline int64_t npkitTicksToNs(uint64_t ticks, int32_t khz) {
+  const uint64_t k = (uint64_t)khz;
+  return (int64_t)((ticks / k) * 1000000ull + (ticks % k) * 1000000ull / k);
+}
 constexpr int kNpkitDevBuffers = 216;  // MSCCL_MAX_NUM_THREAD_BLOCKS: buffer = thread block
 
 // LL FIFO line (ncclLLFifoLine, devcomm.h:35-48): two 8-B {4-B data, 4-B flag} granules.
@@ -113,7 +120,8 @@ struct DevRecvConn {
   uint64_t tailSeen;            // last Simple tail value read (data known present below it)
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
-  int32_t pad[2];
+  int32_t remote;               // sender on another GPU: system-scope acquire after a tail is seen
+  int32_t pad;
 };
 static_assert(sizeof(DevSendConn) == 64 && sizeof(DevRecvConn) == 64, "connection records are four 16-B units");
 
@@ -222,6 +230,10 @@ LaunchFn getSmallLaunchFn(int dtype, int redop);  // mscclSmallKernel (LL, Sum..
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):
 // NPKit's host/GPU clock calibration.  Returns 0 on a successful launch.
 int launchClockProbe(uint64_t* hostWord, void* stream);
+// 16-B line atomicity probe (kernels_probe.hip, mscclAmdLineTearProbe)
+int launchLineWriter(void* lines, int nLines, int iters, int blocks, void* stream);
+int launchLineReader(const void* lines, int nLines, int iters, uint64_t ticks, unsigned long long* out, int blocks,
+                     void* stream);
 
 }  // namespace msccl
 

@@ -199,7 +199,12 @@ struct Interp {
     __syncthreads();
     headSeen = uni(sh->seen[0]);
   }
-  // Simple data: the sender has posted step recvStep once tail > recvStep
+  // Simple data: the sender has posted step recvStep once tail > recvStep.  The lane that sees
+  // the tail issues the acquire that pairs with the sender's release before its tail post
+  // (simpleOp): agent scope for a producer on this GPU, system scope for one on another GPU (its
+  // stores came over xGMI); the workgroup barrier then orders every lane's FIFO loads after it
+  // (MI355X guide, inter-workgroup hand-off: one-lane acquire, s_waitcnt, __syncthreads).  A
+  // step already covered by an earlier tail value was acquired with that value.
   __device__ __forceinline__ void waitRecvTail() {
     if (tailSeen >= recvStep + 1) return;
     if (tid == 0) {
@@ -208,6 +213,8 @@ struct Interp {
       while ((t = atomicLoadSys(rc->tail)) < recvStep + 1) {
         if (spinAbort(spins)) break;
       }
+      if (rc->remote) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      else __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       sh->seen[1] = t;
     }
     __syncthreads();
@@ -765,7 +772,6 @@ struct Interp {
       if (RECV) waitRecvTail();
       if (SEND) waitSendCredit<kFifoSteps>();
       __syncthreads();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
       if (SEND) frs = makeRsrc(sc->simple + (sendStep % kFifoSteps) * (uint64_t)slotBytes);
       for (int base = s0 + tid; base < s1; base += kNT * U) {
@@ -806,15 +812,16 @@ struct Interp {
           if (DST) storePack(drs, vec, B[u], s.n, v[u]);
         }
       }
+      // Hand-off: every lane's FIFO stores (and loads of the slot it frees) complete, the
+      // workgroup barrier, then one lane's release before the tail post (the data) and the head
+      // post (the freed slot): agent scope towards a peer on this GPU, system scope towards
+      // another GPU (the reference's __threadfence_system before postPeer, prims_simple.h:218;
+      // its postPeer stores, prims_simple.h:122-128).  The receiving lane acquires (waitRecvTail).
       drainStores();
       __syncthreads();
       if (tid == 0) {
-        if (SEND && sc->remote) {
-          // FIFO bytes went to another GPU: system-scope release before the tail (the reference's
-          // __threadfence_system before postPeer, prims_simple.h:218)
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-          drainStores();
-        }
+        if ((SEND && sc->remote) || (RECV && rc->remote)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        else __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         if (SEND) atomicStoreSys(sc->remoteTail, sendStep + 1);
         if (RECV) atomicStoreSys(rc->remoteHead, recvStep + 1);
       }
@@ -1070,7 +1077,7 @@ struct Interp {
       nkBuf = lg->events + (size_t)bid * nkCap;
       nkHeadG = lg->heads + bid;
       nkHead = uni(*nkHeadG);
-      nk(NPKIT_EVENT_TIME_SYNC_CPU, 0, (uint64_t)((int64_t)t0 * lg->nsPerTick + lg->cpuOffsetNs));
+      nk(NPKIT_EVENT_TIME_SYNC_CPU, 0, (uint64_t)(npkitTicksToNs(t0, lg->clockKHz) + lg->cpuOffsetNs));
       nk(NPKIT_EVENT_TIME_SYNC_GPU, 0, t0);
     }
 

@@ -127,14 +127,39 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   return s;
 }
 
+// The environment variables behind the Knobs fields in which a and b differ.
+static std::string knobDiff(const Knobs& a, const Knobs& b) {
+  std::string out;
+  auto add = [&](bool differ, const char* name) {
+    if (differ) out += std::string(out.empty() ? "" : ", ") + name;
+  };
+  add(a.mscclOn != b.mscclOn || a.ringOn != b.ringOn || a.treeOn != b.treeOn, "NCCL_ALGO");
+  add(memcmp(a.protoOn, b.protoOn, sizeof(a.protoOn)) != 0, "NCCL_PROTO");
+  add(a.nthreads != b.nthreads, "NCCL_NTHREADS");
+  add(a.ll128Nthreads != b.ll128Nthreads, "NCCL_LL128_NTHREADS");
+  add(a.buffSizes[0] != b.buffSizes[0], "NCCL_LL_BUFFSIZE");
+  add(a.buffSizes[1] != b.buffSizes[1], "NCCL_LL128_BUFFSIZE");
+  add(a.buffSizes[2] != b.buffSizes[2], "NCCL_BUFFSIZE");
+  add(a.ringChannels != b.ringChannels, "MSCCL_AMD_RING_CHANNELS");
+  add(a.split != b.split, "MSCCL_AMD_SPLIT");
+  add(a.targetWgs != b.targetWgs, "MSCCL_AMD_TARGET_WGS");
+  add(a.merge != b.merge, "MSCCL_AMD_MERGE");
+  add(a.ringFallback != b.ringFallback, "MSCCL_AMD_RING_FALLBACK");
+  add(a.ll128Remote != b.ll128Remote, "MSCCL_AMD_LL128_REMOTE");
+  add(a.treeMaxBytes != b.treeMaxBytes, "MSCCL_AMD_TREE_MAX_BYTES");
+  add(a.smallKernel != b.smallKernel, "MSCCL_AMD_SMALL_KERNEL");
+  add(a.referenceSelection != b.referenceSelection, "MSCCL_AMD_REFERENCE_SELECTION");
+  add(a.fuse != b.fuse, "MSCCL_AMD_FUSE");
+  return out.empty() ? "(unnamed field)" : out;
+}
+
 ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   Knobs agreed = comm->knobs;
   agreed.smallKernel = 0;
   for (size_t r = 0; r < recs.size(); r++) {
     if (memcmp(&recs[r].knobs, &agreed, sizeof(Knobs)) != 0) {
-      WARN("MSCCL: rank %zu runs with different NCCL_*/MSCCL_AMD_* settings than rank %d (NCCL_ALGO, NCCL_PROTO, "
-           "NCCL_NTHREADS, NCCL_*BUFFSIZE, MSCCL_AMD_SPLIT/MERGE/TARGET_WGS/RING_CHANNELS/RING_FALLBACK/LL128_REMOTE "
-           "must agree)", r, comm->rank);
+      WARN("MSCCL: rank %zu runs with different settings than rank %d: %s (they shape the FIFO steps and must "
+           "agree across ranks)", r, comm->rank, knobDiff(recs[r].knobs, agreed).c_str());
       return ncclInvalidUsage;
     }
     if (recs[r].nAlgos != (int32_t)comm->algos.size()) {

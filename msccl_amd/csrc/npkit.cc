@@ -36,10 +36,10 @@ int64_t hostNs() {  // the reference's CPU timestamp: system_clock nanoseconds (
       .count();
 }
 
-// Offset such that host ns = ticks * nsPerTick + offset.  The probe kernel stores the GPU clock
+// Offset such that host ns = npkitTicksToNs(ticks, khz) + offset.  The probe kernel stores the GPU clock
 // to host-mapped memory; the host sees it at most a PCIe write later, so every sample
 // over-estimates the offset by that latency and the smallest sample is kept.
-ncclResult_t calibrate(int nsPerTick, int64_t* offset) {
+ncclResult_t calibrate(int khz, int64_t* offset) {
   uint64_t* word = nullptr;
   NCCLCHECK(hipErr(hipHostMalloc((void**)&word, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   hipStream_t s;
@@ -65,7 +65,7 @@ ncclResult_t calibrate(int nsPerTick, int64_t* offset) {
     }
     if (res != ncclSuccess) break;
     const int64_t seen = hostNs();
-    best = std::min(best, seen - (int64_t)t * nsPerTick);
+    best = std::min(best, seen - npkitTicksToNs(t, khz));
     hipStreamSynchronize(s);
   }
   hipStreamSynchronize(s);
@@ -92,8 +92,8 @@ ncclResult_t npkitSetup(ncclComm* comm) {
   NpkitLog lg;
   memset(&lg, 0, sizeof(lg));
   lg.cap = (int32_t)cap;
-  lg.nsPerTick = std::max(1, 1000000 / khz);
-  NCCLCHECK(calibrate(lg.nsPerTick, &lg.cpuOffsetNs));
+  lg.clockKHz = khz;
+  NCCLCHECK(calibrate(khz, &lg.cpuOffsetNs));
   const size_t evBytes = (size_t)kNpkitDevBuffers * cap * sizeof(NpkitEvent);
   NCCLCHECK(hipErr(hipMalloc(&comm->dNpkitEvents, evBytes), "hipMalloc npkit events"));
   NCCLCHECK(hipErr(hipMalloc(&comm->dNpkitHeads, kNpkitDevBuffers * sizeof(uint64_t)), "hipMalloc npkit heads"));

@@ -222,6 +222,7 @@ static ncclResult_t buildConns(ncclComm* comm, int group, int nTb, const std::ve
         c.remoteHead = (uint64_t*)(peerBases[p] + theirs.sendHead + s * theirs.wordStride);
         c.llSlotLines = comm->llSlotLines;
         c.simpleSlotBytes = comm->simpleSlotBytes;
+        c.remote = peerRemote[p];
       }
     }
   }
@@ -450,6 +451,30 @@ std::vector<FuseCandidate> fusableTbs(const Algorithm& a) {
   return out;
 }
 
+// Transfers i, i + 1 of a program are an `s` and a `cpy` of the same source chunks that one
+// copy-send pass may replace: no flag published between them, and the copy's destination chunks
+// either are its source chunks (a self-copy writes back the values it read) or share none with
+// them, so the bytes sent never depend on the order of the pass's loads and stores (the unfused
+// s sends the source before the cpy writes).  Buffers i and o alias in an in-place call (the
+// same memory for AllReduce, one block of it for ReduceScatter / AllGather), so there i and o
+// count as one buffer for AllReduce and a cpy between them is not fused for the others.
+bool sendCopyFusable(const Algorithm& a, const std::vector<Transfer>& ts, size_t i) {
+  if (i + 1 >= ts.size()) return false;
+  const Transfer &s = ts[i], &c = ts[i + 1];
+  if (s.type != kSend || c.type != kLocalCopy || s.srcbuf != c.srcbuf || s.srcoff != c.srcoff ||
+      s.count != c.count || s.hasDep != 0 || c.numDeps != 0)
+    return false;
+  const bool io = c.srcbuf != kScratch && c.dstbuf != kScratch;
+  bool sameBuf = c.srcbuf == c.dstbuf;
+  if (!sameBuf && a.inPlace && io) {
+    if (a.coll != kAllReduce) return false;
+    sameBuf = true;
+  }
+  if (!sameBuf) return true;
+  const int s0 = c.srcoff, s1 = c.srcoff + c.count, d0 = c.dstoff, d1 = c.dstoff + c.count;
+  return (s0 == d0) || s1 <= d0 || d1 <= s0;
+}
+
 // Pack every algorithm's per-tb programs into fixed-stride images and upload them (replaces
 // the 29 MB mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 ncclResult_t algoUpload(ncclComm* comm) {
@@ -481,10 +506,7 @@ ncclResult_t algoUpload(ncclComm* comm) {
       // s followed by a cpy of the same source chunks (an out-of-place AllGather's own block):
       // one copy-send pass reads the source once.  A local change: the FIFO steps are the s's.
       for (size_t i = 0; comm->knobs.fuse && i + 1 < ts.size(); i++)
-        if (ts[i].type == kSend && ts[i + 1].type == kLocalCopy && ts[i].srcbuf == ts[i + 1].srcbuf &&
-            ts[i].srcoff == ts[i + 1].srcoff && ts[i].count == ts[i + 1].count && ts[i].hasDep == 0 &&
-            ts[i + 1].numDeps == 0)
-          ts[i].type = kSendCopy;
+        if (sendCopyFusable(a, ts, i)) ts[i].type = kSendCopy;
       putImage(img, (size_t)b * stride, h, ts, tb.depBid, tb.depStep, tb.redSrcOff);
     }
     NCCLCHECK(uploadImages(img, &d));

@@ -290,15 +290,61 @@ def allreduce_ring(n: int, channels: int = 1, proto: str = "Simple", inplace: bo
 
 def reduce_scatter_allpairs(n: int, instances: int = 1, proto: str = "Simple", inplace: bool = False,
                             min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
-                            nthreads: Optional[int] = None, name: str = "reduce_scatter_pairs") -> str:
-    """All-pairs ReduceScatter.  Input = n blocks of I chunks (block p -> rank p), output = I chunks.
-    n > 2: every peer's copy lands in scratch (one thread block per peer, all links at once) and a
-    reduce thread block folds them.  n == 2: thread block k sends the peer's chunk and receives its
-    own with `rrc` (reduce with the local chunk, write the output): no scratch and no `re`, 5 B of
-    HBM traffic per output byte instead of 7 B."""
+                            nthreads: Optional[int] = None, name: str = "reduce_scatter_pairs",
+                            form: str = "chain") -> str:
+    """All-pairs ReduceScatter.  Input = n blocks (block q -> rank q), output = one block.
+
+    form "chain" (default, no scratch): one thread block per (instance, peer), all links busy at
+    once.  Each output chunk of instance k is cut into P pieces, P the smallest power of two >= n - 1
+    (so sizes divide as the reference's power-of-two loops do).  Thread block (k, p_i) (p_i the i-th
+    peer in ascending order) runs P stages; at stage t it works on piece j = (i - t) mod P: `s` of
+    the piece its peer works on at stage t, then `rrc` of piece j, receiving peer p_i's copy and
+    reducing it with the partial sum the piece's previous fold left in the output (a dependency on
+    that thread block's stage; the first fold of a piece starts from the rank's own input block).
+    Every (thread block, piece) pair meets at exactly one stage, so each piece is folded once per
+    peer and every thread block is busy at every stage: the chain is pipelined over pieces.  Per
+    piece the fold is ((x_r (+) x_a) (+) x_b) ... over the peers in the order their stages come,
+    fn(local, peer) for Simple, fn(peer, local) for LL (oracle/sim.py runs the same program).  HBM
+    bytes per output byte: 5 (n - 1), against 5 n + 1 for the scratch form.  For n = 2 it is one
+    `s` + `rrc` per thread block (P = 1).
+    form "scratch": every peer's copy lands in scratch (one thread block per peer) and a reduce
+    thread block folds them with one fused `re` (own block first: (s0 (+) s1 ...) (+) d for Simple)."""
     I = instances
-    ncpl = n * I
     gpus = {}
+    if form == "chain":
+        P = 1
+        while P < n - 1:
+            P *= 2
+        ncpl = n * I * P
+        for r in range(n):
+            peers = [p for p in range(n) if p != r]
+            tid = {(k, i): k * (n - 1) + i for k in range(I) for i in range(n - 1)}
+            # folds of piece j: (stage, tb index) in stage order
+            folds = {j: sorted(((i - j) % P, i) for i in range(n - 1)) for j in range(P)}
+            tbs = []
+            for k in range(I):
+                for i, p in enumerate(peers):
+                    tb = _Tb(tid[(k, i)], p, p, k)
+                    ip = _slot_of(r, p)  # my index among p's peers
+                    for t in range(P):
+                        js = (ip - t) % P        # the piece of block p that p folds at stage t
+                        tb.add("s", "i", p * I * P + k * P + js, "o", k * P + js, 1)
+                        j = (i - t) % P
+                        f = folds[j].index((t, i))
+                        src = ("i", r * I * P + k * P + j) if f == 0 else ("o", k * P + j)
+                        dep = (-1, -1)
+                        if f > 0:
+                            tp, ipv = folds[j][f - 1]
+                            dep = (tid[(k, ipv)], 2 * tp + 1)
+                        tb.add("rrc", src[0], src[1], "o", k * P + j, 1, dep[0], dep[1], int(f < n - 2))
+                    tbs.append(tb)
+            gpus[r] = (ncpl, I * P, 0, tbs)
+        if max_bytes is None:
+            max_bytes = 1 << 62
+        return _emit(name, proto, I, ncpl, n, "reduce_scatter", inplace, gpus, min_bytes, max_bytes, nthreads)
+    if form != "scratch":
+        raise ValueError("form must be 'chain' or 'scratch'")
+    ncpl = n * I
     if n == 2:
         for r in range(2):
             p = 1 - r

@@ -33,7 +33,7 @@ CASES = [
      7, 0, False, "uniform"),
     ("ring8_simple_bf16", lambda: xmlgen.allreduce_ring(8, 4, "Simple"), 8, L.ALLREDUCE, 4096, 9, 0, True, "uniform"),
     ("ring4_ll_f32_max", lambda: xmlgen.allreduce_ring(4, 2, "LL"), 4, L.ALLREDUCE, 800, 7, 2, True, "uniform"),
-    ("rs8_simple_f32", lambda: xmlgen.reduce_scatter_allpairs(8, 2, "Simple"), 8, L.REDUCE_SCATTER, 512, 7, 0,
+    ("rs8_simple_f32", lambda: xmlgen.reduce_scatter_allpairs(8, 2, "Simple", form="scratch"), 8, L.REDUCE_SCATTER, 512, 7, 0,
      False, "uniform"),
     ("ag8_ll_f32", lambda: xmlgen.allgather_allpairs(8, 2, "LL"), 8, L.ALLGATHER, 512, 7, 0, False, "uniform"),
     ("ap2_ll_i32_exact", lambda: xmlgen.allreduce_allpairs(2, 2, "LL"), 2, L.ALLREDUCE, 1024, 2, 0, True, "exact"),

@@ -62,15 +62,18 @@ def gen_inputs(n: int, count: int, dt: int, seed: int, mode: str = "uniform") ->
 
 def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, op: int = 0,
                    in_place: bool = True, seed: int = 1, mode: str = "uniform", iters: int = 1,
-                   tmpdir: str = "/tmp", extra_xmls: Optional[List[str]] = None):
-    """Returns (gpu_outputs, oracle_outputs) as lists of numpy arrays (interpreter element type)."""
+                   tmpdir: str = "/tmp", extra_xmls: Optional[List[str]] = None,
+                   devices: Optional[List[int]] = None):
+    """Returns (gpu_outputs, oracle_outputs) as lists of numpy arrays (interpreter element type).
+    devices: the device of each rank (default: all on cuda:0, co-resident)."""
     import torch
     path = os.path.join(tmpdir, "msccl_test_%d_%d.xml" % (os.getpid(), abs(hash(xml_text)) % 100000))
     with open(path, "w") as f:
         f.write(xml_text)
     os.environ["MSCCL_XML_FILES"] = ":".join([path] + (extra_xmls or []))
-    dev = torch.device("cuda:0")
-    comms = M.Comm.init_all([0] * nranks)
+    devices = list(devices) if devices is not None else [0] * nranks
+    devs = [torch.device("cuda", d) for d in devices]
+    comms = M.Comm.init_all(devices)
     try:
         algos = [L.parse_xml(xml_text, r, nranks) for r in range(nranks)]
         ts = N.type_size(dt)
@@ -82,7 +85,7 @@ def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, o
             in_n, out_n = count, count * nranks
         ins = gen_inputs(nranks, in_n, dt, seed, mode)
         # GPU
-        t_in = [to_torch(x, dev) for x in ins]
+        t_in = [to_torch(x, devs[r]) for r, x in enumerate(ins)]
         if in_place:
             if coll == L.ALLREDUCE:
                 t_out = t_in
@@ -93,27 +96,29 @@ def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, o
                 sends = [t.data_ptr() for t in t_in]
                 recvs = [t.data_ptr() for t in t_out]
             else:
-                t_out = [torch.zeros(out_n, dtype=t_in[0].dtype, device=dev) for _ in range(nranks)]
+                t_out = [torch.zeros(out_n, dtype=t_in[0].dtype, device=devs[r]) for r in range(nranks)]
                 for r in range(nranks):
                     t_out[r][r * count:(r + 1) * count] = t_in[r]
                 sends = [t_out[r][r * count:(r + 1) * count].data_ptr() for r in range(nranks)]
                 recvs = [t.data_ptr() for t in t_out]
         else:
-            t_out = [torch.full((out_n,), 7, dtype=t_in[0].dtype, device=dev) for _ in range(nranks)]
+            t_out = [torch.full((out_n,), 7, dtype=t_in[0].dtype, device=devs[r]) for r in range(nranks)]
             sends = [t.data_ptr() for t in t_in]
             recvs = [t.data_ptr() for t in t_out]
-        torch.cuda.synchronize()
-        stream = torch.cuda.current_stream().cuda_stream
+        for d in set(devs):
+            torch.cuda.synchronize(d)
+        streams = [torch.cuda.current_stream(d).cuda_stream for d in devs]
         for _ in range(iters):
             with M.group():
                 for r, c in enumerate(comms):
                     if coll == L.ALLREDUCE:
-                        c.all_reduce(sends[r], recvs[r], count, dt, op, stream)
+                        c.all_reduce(sends[r], recvs[r], count, dt, op, streams[r])
                     elif coll == L.REDUCE_SCATTER:
-                        c.reduce_scatter(sends[r], recvs[r], count, dt, op, stream)
+                        c.reduce_scatter(sends[r], recvs[r], count, dt, op, streams[r])
                     else:
-                        c.all_gather(sends[r], recvs[r], count, dt, stream)
-        torch.cuda.synchronize()
+                        c.all_gather(sends[r], recvs[r], count, dt, streams[r])
+        for d in set(devs):
+            torch.cuda.synchronize(d)
         for c in comms:
             err = c.async_error()
             if err != 0:

@@ -58,6 +58,11 @@ def main():
     prof = os.path.join(root, "profiles")
     os.makedirs(prof, exist_ok=True)
     res = {"tag": tag}
+    # the device sources this profile was taken on (bench.py uses a committed profile's traffic
+    # only for the same kernel_src_hash)
+    sys.path.insert(0, root)
+    import bench
+    res["kernel_src"] = bench.kernel_src_hash()
     stats = find(os.path.join(out, "kt"), "*kernel_stats.csv")
     if stats:
         shutil.copy(stats[0], os.path.join(prof, tag + "_kernel_stats.csv"))
