@@ -24,7 +24,8 @@ constexpr uint64_t kCommMagic = 0x6d7363636c616d64ull;  // "msccl amd"
 // fallback's channels.  Every group owns its connections (transport.cc).
 constexpr int kRingGroup = kMaxAlgos;
 constexpr int kTreeGroup = kMaxAlgos + 1;  // the tree fallback's chain connections
-constexpr int kNumGroups = kMaxAlgos + 2;
+constexpr int kFlatGroup = kMaxAlgos + 2;  // the flat tree's all-pairs connections (channel 0)
+constexpr int kNumGroups = kMaxAlgos + 3;
 struct ConnKey {
   int group, chan, peer;
 };
@@ -66,7 +67,7 @@ struct ncclComm {
   std::vector<msccl::Algorithm> algos;
   std::vector<msccl::Registration> regs;
   std::vector<msccl::DevAlgoHost> devAlgos;
-  msccl::DevAlgoHost ringAlgos[5];  // ring fallback programs, [4] = tree (transport.cc: ringUpload)
+  msccl::DevAlgoHost ringAlgos[6];  // ring fallback programs, [4] = tree, [5] = flat tree (transport.cc: ringUpload)
   msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank
   bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank
   bool anyRemote = false;          // some peer runs on another GPU (xGMI): no LL128 unless allowed
@@ -89,6 +90,10 @@ struct ncclComm {
   msccl::DevRecvConn* ringRecv = nullptr;
   msccl::DevSendConn* treeSend = nullptr;              // tree fallback connections [2 * kRingChannels]
   msccl::DevRecvConn* treeRecv = nullptr;
+  msccl::DevSendConn* flatSend = nullptr;              // flat tree connections [nRanks] (tb 0 has none)
+  msccl::DevRecvConn* flatRecv = nullptr;
+  void* flatScratch = nullptr;                         // flat tree: nRanks slots of a call's bytes
+  size_t flatScratchBytes = 0;
   int llSlotLines = 0, simpleSlotBytes = 0;
   int buffSizes[3] = {0, 0, 0};
 

@@ -158,7 +158,10 @@ struct DevComm {
 // Ring / tree fallback kinds (RankWork::ringColl).  kTreeAllReduce: the reference's tree
 // AllReduce (all_reduce.h:103-298) on a chain, two thread blocks per channel (reduce up /
 // broadcast down, as runTreeSplit), offsets gridOffset + channel * chunkSize.
-enum : int { kRingNone = 0, kRingAllReduce = 1, kRingReduceScatter = 2, kRingAllGather = 3, kTreeAllReduce = 4 };
+// kTreeFlat is a host-side plan kind only: the flat tree runs as an MSCCL schedule (ringColl 0 in
+// its RankWork, plan.cc: makeFlatTreePlan).
+enum : int { kRingNone = 0, kRingAllReduce = 1, kRingReduceScatter = 2, kRingAllGather = 3, kTreeAllReduce = 4,
+             kTreeFlat = 5 };
 
 // One rank's share of a launch (the reference passes ncclDevComm* + a 64-B ncclWorkElem,
 // common.h:263-266; here the whole descriptor rides in the kernel argument block).

@@ -92,8 +92,11 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
   if (idx < 0) {
     // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
     if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
-      INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; ring fallback (%s, %d channels)",
-           op.coll, op.count, (int)op.dtype, out->plan.proto == kProtoLL ? "LL" : "Simple", out->plan.ringChannels);
+      if (comm->flatScratch) makeFlatTreePlan(c, comm->knobs, comm->flatScratchBytes, &out->plan);
+      INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; %s fallback (%s, %d channels)",
+           op.coll, op.count, (int)op.dtype,
+           out->plan.ringColl == kTreeFlat ? "flat tree" : out->plan.ringColl == kTreeAllReduce ? "tree" : "ring",
+           out->plan.proto == kProtoLL ? "LL" : "Simple", out->plan.ringChannels);
       return ncclSuccess;
     }
     WARN("MSCCL: no loaded algorithm matches coll=%d count=%zu type=%d op=%d inplace=%d nranks=%d "
@@ -124,6 +127,7 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
     // happens when MSCCL_AMD_MAX_SCRATCH capped it.  The reference reports ncclInternalError
     // (enqueue.cc:580-589); the capped schedule is treated as not matching instead.
     if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
+      if (comm->flatScratch) makeFlatTreePlan(c, comm->knobs, comm->flatScratchBytes, &out->plan);
       INFO(kSubColl, "MSCCL: scratch %zu < %zu needed (MSCCL_AMD_MAX_SCRATCH); ring fallback", comm->scratchSize,
            out->plan.scratchNeeded);
       return ncclSuccess;
@@ -180,7 +184,53 @@ RankWork makeRingWork(Planned& p) {
   return w;
 }
 
+// Flat tree (plan.cc: makeFlatTreePlan): the program of transport.cc's ringUpload (ringAlgos[5])
+// run as an MSCCL schedule (ringColl 0 on the device), so one-iteration calls take the small kernel.
+RankWork makeFlatWork(Planned& p) {
+  ncclComm* comm = p.op.comm;
+  const DevAlgoHost& da = comm->ringAlgos[5];
+  RankWork w;
+  memset(&w, 0, sizeof(w));
+  w.sendbuff = p.op.sendbuff;
+  w.recvbuff = p.op.recvbuff;
+  w.scratch = comm->flatScratch;
+  w.comm = comm->dComm;
+  w.send = da.dSend;
+  w.recv = da.dRecv;
+  w.connSplit = 1;
+  w.images = da.dImages;
+  w.tbStride = da.tbStride;
+  w.timeoutTicks = comm->timeoutTicks;
+  w.llFlagMask = comm->llFlagMask;
+  w.llCleanMask = comm->llCleanMask;
+  w.trace = comm->dTrace;
+  w.traceEvents = comm->traceEvents;
+  w.npkit = comm->dNpkit;
+  w.flags = comm->dFlags;
+  w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  w.maxSplit = comm->maxSplit;
+  w.sizePerChunk = p.plan.sizePerChunk;
+  w.chunkSize = p.plan.chunkSize;
+  w.minChunk = p.plan.minChunk;
+  w.split = 1;
+  w.nBlocks = (int16_t)da.nBlocks;
+  const int64_t pe = 16 / refTypeSize(p.plan.dtype);
+  w.maxOpElems = (int64_t)kMaxRunSlots * (comm->llSlotLines / 2) * pe;
+  int merge = 1;
+  if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {  // makeWork's rule, send runs of one chunk
+    const int64_t chunk = std::max<int64_t>(1, p.plan.chunkSize);
+    merge = (int)std::max<int64_t>(1, std::min<int64_t>(64, w.maxOpElems / chunk));
+  }
+  w.merge = (uint8_t)merge;
+  w.refNthreads = (int16_t)p.plan.refNthreads;
+  w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
+  w.launchSeq = comm->workIndex++;
+  comm->last = {-1, p.plan.proto, 1, merge, kTreeFlat, 0, w.nBlocks};
+  return w;
+}
+
 RankWork makeWork(Planned& p) {
+  if (p.plan.ringColl == kTreeFlat) return makeFlatWork(p);
   if (p.plan.ringColl) return makeRingWork(p);
   ncclComm* comm = p.op.comm;
   const DevAlgoHost& da = comm->devAlgos[p.plan.algoIndex];
@@ -274,11 +324,12 @@ bool smallEligible(const Planned& p, const RankWork& w) {
   const int64_t sp = p.plan.sizePerChunk, cs = p.plan.chunkSize;
   const int64_t k = cs > 0 ? sp / cs : 0, m = std::min<int64_t>(std::max<int>(1, w.merge), std::max<int64_t>(1, k));
   const bool onePass = sp <= cs || (cs > 0 && sp % cs == 0 && k % m == 0);
-  return comm->knobs.smallKernel && p.plan.ringColl == 0 && p.plan.proto == kProtoLL && p.op.devOp <= 3 &&
-         onePass && (w.trace == nullptr || comm->traceLight) && w.npkit == nullptr &&
+  const bool flat = p.plan.ringColl == kTreeFlat;
+  const int64_t chunks = flat ? comm->nRanks : maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop);
+  return comm->knobs.smallKernel && (p.plan.ringColl == 0 || flat) && p.plan.proto == kProtoLL &&
+         p.op.devOp <= 3 && onePass && (w.trace == nullptr || comm->traceLight) && w.npkit == nullptr &&
          (w.split & (w.split - 1)) == 0 &&
-         p.plan.sizePerChunk * maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop) *
-                 refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit element offsets
+         p.plan.sizePerChunk * chunks * refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit offsets
 }
 
 ncclResult_t launchGroup(std::vector<Planned*>& ps) {

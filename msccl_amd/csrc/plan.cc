@@ -79,6 +79,7 @@ Knobs Knobs::fromEnv() {
   k.treeMaxBytes = envInt("MSCCL_AMD_TREE_MAX_BYTES", -1);  // -1: 16 KiB per rank (makeRingPlan)
   k.smallKernel = envInt("MSCCL_AMD_SMALL_KERNEL", 1) != 0;
   k.fuse = envInt("MSCCL_AMD_FUSE", 1) != 0;
+  k.treeFlat = envInt("MSCCL_AMD_TREE_FLAT", 1) != 0;
   return k;
 }
 
@@ -238,6 +239,29 @@ static int makeTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   p->chunkSize = chunk;
   p->minChunk = minChunk;
   p->ringColl = kTreeAllReduce;
+  return 0;
+}
+
+int makeFlatTreePlan(const CallDesc& c, const Knobs& k, size_t scratchBytes, Plan* p) {
+  if (!k.treeFlat || p->ringColl != kTreeAllReduce || p->proto != kProtoLL || c.redop > kDevMin ||
+      c.nRanks < 2 || c.nRanks > kMaxReduceFusion || (size_t)p->nBytes * c.nRanks > scratchBytes)
+    return 1;
+  // The program (transport.cc: flatProgram) is an MSCCL schedule with one chunk per loop: input
+  // chunk 0, scratch chunks 0..n-1.  Chunk math of makePlan for LL (enqueue.cc:591-734,
+  // msccl_interpreter.h:79-86) with nchunksPerLoop 1 and the tree's thread count.
+  const int ts = refTypeSize(p->dtype);
+  const int nt = p->refNthreads;
+  const int64_t stepSize = k.buffSizes[kProtoLL] / kFifoSteps;
+  p->ringColl = kTreeFlat;
+  p->ringChannels = 0;
+  p->nchunksPerLoop = 1;
+  p->sizeMultiplier = 1;
+  p->maxAllowedCount = (int)std::min<int64_t>(kMaxCount - 1, std::max<int64_t>(1, (stepSize / 2) / std::max<int64_t>(1, p->nBytes)));
+  p->chunkSize = (int64_t)(int)(stepSize / 2 / ts);
+  p->minChunk = std::max<int64_t>(1, (int64_t)nt * (8 / ts));
+  p->sizePerChunk = p->count;
+  p->nIters = (int)((p->sizePerChunk + p->chunkSize - 1) / p->chunkSize);
+  p->scratchNeeded = (size_t)p->nBytes * c.nRanks;
   return 0;
 }
 

@@ -69,7 +69,7 @@ struct Knobs {
   int32_t smallKernel;       // MSCCL_AMD_SMALL_KERNEL: one-iteration LL launches take mscclSmallKernel
   int32_t referenceSelection;  // MSCCL_AMD_REFERENCE_SELECTION: the reference's MSCCL gating (below)
   int32_t fuse;              // MSCCL_AMD_FUSE: fused s + rrc exchanges (transport.cc: fusableTbs)
-  int32_t pad;               // no implicit padding (Knobs are compared with memcmp)
+  int32_t treeFlat;          // MSCCL_AMD_TREE_FLAT: the tree's values in one hop (plan.cc: makeFlatTreePlan)
   static Knobs fromEnv();
 };
 
@@ -92,5 +92,11 @@ int chooseSplit(int maxBlocks, int coResident, const Knobs& k);
 // 0, or returns ncclInvalidUsage when the collective / op has no ring (AllToAll, custom, Avg).
 // Channels, protocol and thread count are this build's choice (oracle/ring.py: ring_params).
 int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p);
+// The flat tree (kTreeFlat): a tree AllReduce plan (makeRingPlan chose the tree, LL, op Sum..Min,
+// 2..16 ranks) turned into a one-iteration-per-chunk MSCCL plan of the flat program
+// (transport.cc: flatProgram): every rank sends its input to every peer's scratch slot and folds
+// the n slots in the chain tree's order x_{n-1} (+) x_{n-2} (+) ... (+) x_0, one hop instead of
+// 2 (n - 1).  Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).
+int makeFlatTreePlan(const CallDesc& c, const Knobs& k, size_t scratchBytes, Plan* p);
 
 }  // namespace msccl

@@ -32,6 +32,7 @@ size_t alignUp(size_t x, size_t a) { return (x + a - 1) / a * a; }
 // Protocols whose FIFO memory a group needs (LL and LL128 share the LL FIFO).
 uint8_t groupProtoMask(const ncclComm* comm, int group) {
   if (group == kRingGroup || group == kTreeGroup) return (uint8_t)((1u << kProtoLL) | (1u << kProtoSimple));
+  if (group == kFlatGroup) return (uint8_t)(1u << kProtoLL);
   uint8_t m = (uint8_t)(1u << comm->algos[group].proto);
   for (auto& r : comm->regs)
     if (r.algoIndex == group) m |= (uint8_t)(1u << r.proto);
@@ -40,7 +41,7 @@ uint8_t groupProtoMask(const ncclComm* comm, int group) {
 }
 
 int groupSubs(const ncclComm* comm, int group) {
-  if (group == kRingGroup || group == kTreeGroup) return 1;  // the ring and the tree run unsplit
+  if (group == kRingGroup || group == kTreeGroup || group == kFlatGroup) return 1;  // the fallbacks run unsplit
   return comm->algoSplit.empty() ? 1 : comm->algoSplit[group];
 }
 // The tree fallback's chain (rank order, root 0): thread block 2c+0 reduces up (receives from
@@ -61,6 +62,21 @@ void treePeers(int rank, int n, std::vector<int>* sp, std::vector<int>* rp) {
       (*sp)[2 * c + 1] = child;
     }
   }
+}
+// The flat tree's thread blocks: 0 folds (no peer), 1 + j exchanges with the j-th peer in
+// ascending rank order (sends to it and receives from it, channel 0).
+void flatPeers(int rank, int n, std::vector<int>* sp, std::vector<int>* rp) {
+  sp->assign(n, -1);
+  rp->assign(n, -1);
+  for (int j = 0, b = 1; j < n; j++)
+    if (j != rank) {
+      (*sp)[b] = j;
+      (*rp)[b] = j;
+      b++;
+    }
+}
+bool flatEnabled(const ncclComm* comm) {
+  return comm->ringFallback && comm->knobs.treeFlat && comm->nRanks > 1 && comm->nRanks <= kMaxReduceFusion;
 }
 }  // namespace
 
@@ -131,6 +147,12 @@ ncclResult_t transportPlan(ncclComm* comm) {
       if (rp[b] >= 0) comm->recvKeys.push_back(ConnKey{kTreeGroup, b / 2, rp[b]});
     }
   }
+  if (flatEnabled(comm))
+    for (int p = 0; p < n; p++)
+      if (p != comm->rank) {
+        comm->sendKeys.push_back(ConnKey{kFlatGroup, 0, p});
+        comm->recvKeys.push_back(ConnKey{kFlatGroup, 0, p});
+      }
   const int64_t llBytes = (int64_t)alignUp((size_t)kLLFifoSlots * comm->llSlotLines * 16, kFifoAlign);
   const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
   comm->table.assign((size_t)kNumGroups * kMaxChannels * n,
@@ -261,6 +283,12 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
     for (int b = 0; b < 2 * kRingChannels; b++) tch[b] = b / 2;
     NCCLCHECK(buildConns(comm, kTreeGroup, 2 * kRingChannels, tsp, trp, tch, tables, peerBases, peerRemote,
                          &comm->treeSend, &comm->treeRecv));
+  }
+  if (flatEnabled(comm)) {
+    std::vector<int> fsp, frp, fch(n, 0);
+    flatPeers(comm->rank, n, &fsp, &frp);
+    NCCLCHECK(buildConns(comm, kFlatGroup, n, fsp, frp, fch, tables, peerBases, peerRemote, &comm->flatSend,
+                         &comm->flatRecv));
   }
   return ncclSuccess;
 }
@@ -403,6 +431,71 @@ ncclResult_t ringUpload(ncclComm* comm) {
       h.hasRecv = rp[b] >= 0;
       h.nsteps = (uint16_t)prog.size();
       putImage(img, (size_t)b * d.tbStride, h, prog, none, none, none);
+    }
+    NCCLCHECK(uploadImages(img, &d));
+  }
+  if (flatEnabled(comm)) {
+    // The flat tree (plan.cc: makeFlatTreePlan), an MSCCL schedule of one chunk per loop:
+    //   tb 1 + j (peer p_j): s i0 -> p_j (its scratch slot r), r from p_j -> scratch slot p_j;
+    //   tb 0: cpy i0 -> scratch slot r; wait for every peer's r; re into slot n - 1 from slots
+    //   n - 2, ..., 0 (LL order: acc = slot n-1, acc = acc (+) slot q, q descending, skipping
+    //   n - 1); cpy slot n - 1 -> o0.
+    // The fold is the chain tree's (runTreeSplit on the chain, transport.cc: treePeers): leaf
+    // n - 1 sends its input up, rank q folds fn(child's partial, x_q), the root's result comes
+    // back down.  Every op admitted (Sum, Prod, Max, Min) is commutative per element, so the
+    // values are the tree's bit for bit, whatever side of fn each operand sits on.
+    const int r = comm->rank;
+    std::vector<int> sp, rp;
+    flatPeers(r, n, &sp, &rp);
+    auto mk = [](uint8_t type, uint8_t sb, int so, uint8_t db, int dof) {
+      Transfer t;
+      t.type = type;
+      t.srcbuf = sb;
+      t.srcoff = (int16_t)so;
+      t.dstbuf = db;
+      t.dstoff = (int16_t)dof;
+      t.count = 1;
+      return t;
+    };
+    std::vector<Transfer> fold;
+    fold.push_back(mk(kLocalCopy, kInput, 0, kScratch, r));
+    Transfer re = mk(kReduce, kScratch, n - 2, kScratch, n - 1);
+    re.numDeps = (int16_t)(n - 1);
+    re.depPtr = 0;
+    re.numReds = (int16_t)(n - 1);
+    re.redPtr = 0;
+    fold.push_back(re);
+    fold.push_back(mk(kLocalCopy, kScratch, n - 1, kOutput, 0));
+    std::vector<int16_t> depBid, depStep, reds;
+    for (int b = 1; b < n; b++) {
+      depBid.push_back((int16_t)b);
+      depStep.push_back(1);   // the peer thread block's r (its transfer 1) publishes step 1
+    }
+    for (int q = n - 2; q >= 0; q--) reds.push_back((int16_t)q);
+    DevAlgoHost& d = comm->ringAlgos[5];
+    d.nBlocks = n;
+    d.tbStride = (int)std::max(imageBytes(fold.size(), depBid.size(), reds.size()), imageBytes(2, 0, 0));
+    d.connSplit = 1;
+    d.dSend = comm->flatSend;
+    d.dRecv = comm->flatRecv;
+    std::vector<char> img((size_t)d.tbStride * n, 0);
+    const std::vector<int16_t> none;
+    for (int b = 0; b < n; b++) {
+      DevTbHeader h;
+      memset(&h, 0, sizeof(h));
+      h.hasSend = sp[b] >= 0;
+      h.hasRecv = rp[b] >= 0;
+      if (b == 0) {
+        h.nsteps = (uint16_t)fold.size();
+        h.ndeps = (uint16_t)depBid.size();
+        h.nreds = (uint16_t)reds.size();
+        putImage(img, 0, h, fold, depBid, depStep, reds);
+      } else {
+        std::vector<Transfer> ex{mk(kSend, kInput, 0, kScratch, r), mk(kRecv, kInput, -1, kScratch, rp[b])};
+        ex[1].hasDep = 1;
+        h.nsteps = 2;
+        putImage(img, (size_t)b * d.tbStride, h, ex, none, none, none);
+      }
     }
     NCCLCHECK(uploadImages(img, &d));
   }

@@ -215,6 +215,7 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
             if c.async_error() != 0:
                 raise M.NcclError(c.async_error(), "kernel (async error)")
         gpu = [from_torch(t, N.storage(dt)) for t in t_out]
+        last = comms[0].info()["last"]   # what the product ran (ringColl 4 chain tree, 5 flat tree)
         if user_scale is not None:
             for c, o in zip(comms, ops):
                 c.destroy_op(o)
@@ -233,6 +234,7 @@ def run_ring_fallback(nranks: int, coll: int, count: int, dt: int, op: int = 0, 
         res, rp = R.run(coll, count, dt, dev_op, o_in, o_out, in_place, arg)
         if iters > 1 and coll == L.ALLREDUCE and in_place:
             o_in = res
+    rp = dict(rp, last=last)
     return gpu, [np.asarray(r) for r in res], rp
 
 

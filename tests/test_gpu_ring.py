@@ -194,3 +194,46 @@ def test_tree_threshold_and_repeats(monkeypatch):
     assert check(4, L.ALLREDUCE, 16384, 7)["algo"] == "tree"
     assert check(4, L.ALLREDUCE, 16385, 7)["algo"] == "ring"
     assert check(4, L.ALLREDUCE, 50000, 7, iters=2)["algo"] == "ring"
+
+
+# ---- flat tree: the chain tree's values in one hop (plan.cc: makeFlatTreePlan) -------------------
+def _flat_env(monkeypatch, tree_max=None):
+    monkeypatch.setenv("NCCL_ALGO", "Ring,Tree")
+    if tree_max is None:
+        monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES")   # default 16 KiB x n per rank
+    else:
+        monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", str(tree_max))
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("count", [1, 37, 511, 512, 4099])
+@pytest.mark.parametrize("dt", [7, 6, 9])
+def test_flat_tree_equals_the_chain_tree(monkeypatch, n, count, dt):
+    """Small AllReduces take the flat tree (all-pairs exchange, fold in the chain's order
+    x_{n-1} (+) ... (+) x_0) in the small kernel; the oracle is oracle/ring.py's chain tree."""
+    _flat_env(monkeypatch)
+    rp = check(n, L.ALLREDUCE, count, dt, seed=5 + n)
+    assert rp["algo"] == "tree"
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 1, rp["last"]
+
+
+@pytest.mark.parametrize("op,dt", [(1, 7), (2, 6), (3, 9), (0, 2), (1, 4), (2, 0)])
+@pytest.mark.parametrize("in_place", [True, False])
+def test_flat_tree_ops(monkeypatch, op, dt, in_place):
+    _flat_env(monkeypatch)
+    rp = check(4, L.ALLREDUCE, 3001, dt, op=op, in_place=in_place, iters=3)
+    assert rp["last"]["ringColl"] == 5, rp["last"]
+
+
+def test_flat_tree_multi_iteration_and_chain_knob(monkeypatch):
+    """Several interpreter iterations (8192 floats each; the general kernel when they do not
+    merge evenly); MSCCL_AMD_TREE_FLAT=0 keeps the chain; Avg (PreMulSum) always takes the chain."""
+    _flat_env(monkeypatch, 256 << 10)
+    rp = check(8, L.ALLREDUCE, 50001, 7, iters=2)
+    assert rp["last"]["ringColl"] == 5, rp["last"]
+    rp = check(8, L.ALLREDUCE, 8192 * 4, 7)
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 1, rp["last"]
+    assert check(4, L.ALLREDUCE, 3001, 7, op=4)["last"]["ringColl"] == 4
+    monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")
+    rp = check(8, L.ALLREDUCE, 4099, 6)
+    assert rp["algo"] == "tree" and rp["last"]["ringColl"] == 4, rp["last"]
