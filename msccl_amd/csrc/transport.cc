@@ -153,8 +153,12 @@ ncclResult_t transportPlan(ncclComm* comm) {
         comm->sendKeys.push_back(ConnKey{kFlatGroup, 0, p});
         comm->recvKeys.push_back(ConnKey{kFlatGroup, 0, p});
       }
-  const int64_t llBytes = (int64_t)alignUp((size_t)kLLFifoSlots * comm->llSlotLines * 16, kFifoAlign);
-  const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign);
+  // MSCCL_AMD_FIFO_PAD (bytes, rounded to 4 KiB; default 0): extra space after every FIFO, so
+  // sub-connections do not start at the same offset modulo the FIFO size (a placement
+  // experiment; each rank publishes its own strides, so ranks need not agree)
+  const int64_t pad = (int64_t)alignUp((size_t)std::max<int64_t>(0, envInt("MSCCL_AMD_FIFO_PAD", 0)), kFifoAlign);
+  const int64_t llBytes = (int64_t)alignUp((size_t)kLLFifoSlots * comm->llSlotLines * 16, kFifoAlign) + pad;
+  const int64_t simpleBytes = (int64_t)alignUp((size_t)kFifoSteps * comm->simpleSlotBytes, kFifoAlign) + pad;
   comm->table.assign((size_t)kNumGroups * kMaxChannels * n,
                      PeerOffsets{-1, -1, -1, -1, llBytes, simpleBytes, (int64_t)kWordStride, 0});
   size_t off = 0;

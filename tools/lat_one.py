@@ -18,15 +18,20 @@ def main():
     ap.add_argument("--proto", default="LL")
     ap.add_argument("--dtype", type=int, default=7)
     ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--graph", action="store_true",
+                    help="capture the launches in one hipGraph and time its replay: device time per launch "
+                         "without the host's per-call cost")
     a = ap.parse_args()
     import torch
     gen = {"allpairs": lambda: xmlgen.allreduce_allpairs(a.ranks, a.instances, a.proto),
            "pair": lambda: xmlgen.allreduce_pair_oneshot(a.instances, a.proto),
            "ring": lambda: xmlgen.allreduce_ring(a.ranks, a.instances, a.proto),
            "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2)}
-    if a.schedule in ("fbring", "fbtree"):   # no schedule: the ring / tree fallback
+    if a.schedule in ("fbring", "fbtree", "fbchain"):   # no schedule: the ring / tree fallback
         os.environ.pop("MSCCL_XML_FILES", None)
         os.environ["NCCL_ALGO"] = "Ring" if a.schedule == "fbring" else "Tree"
+        if a.schedule == "fbchain":   # the chain tree (fbtree: the flat tree where it applies)
+            os.environ["MSCCL_AMD_TREE_FLAT"] = "0"
     else:
         path = "/tmp/lat_one_%d.xml" % os.getpid()
         open(path, "w").write(gen[a.schedule]())
@@ -36,24 +41,39 @@ def main():
     cnt = a.bytes // ts
     bufs = [torch.ones(cnt * ts // 4 + 1, device="cuda") for _ in comms]
 
+    stream = torch.cuda.Stream()
+
     def step():
         with M.group():
             for c, b in zip(comms, bufs):
-                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, 0)
+                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, stream.cuda_stream)
     for _ in range(20):
         step()
     torch.cuda.synchronize()
     import time
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
+    graph = None
+    if a.graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+            for _ in range(a.iters):
+                step()
+        torch.cuda.synchronize()
+    e0.record(stream)
     t0 = time.perf_counter()
-    for _ in range(a.iters):
-        step()
+    if graph is not None:
+        with torch.cuda.stream(stream):
+            graph.replay()
+    else:
+        for _ in range(a.iters):
+            step()
     host = (time.perf_counter() - t0) / a.iters
-    e1.record()
+    e1.record(stream)
     torch.cuda.synchronize()
-    print("%s %d B x%d ranks: %.2f us per launch (events), host %.2f us per call" % (
-        a.schedule, a.bytes, a.ranks, e0.elapsed_time(e1) * 1000 / a.iters, host * 1e6), flush=True)
+    last = comms[0].info()["last"]
+    print("%s %d B x%d ranks: %.2f us per launch (events%s), host %.2f us per call; ran ringColl %d small %d" % (
+        a.schedule, a.bytes, a.ranks, e0.elapsed_time(e1) * 1000 / a.iters, ", graph replay" if graph else "",
+        host * 1e6, last["ringColl"], last["small"]), flush=True)
     for c in comms:
         c.destroy()
 
