@@ -177,7 +177,8 @@ struct RankWork {
   uint64_t* flags;
   uint64_t* epochs;
   int32_t maxSplit;
-  int32_t pad0;
+  int16_t rotate;               // small kernel: workgroup b of the rank runs local slot (b + rotate) % nBlocks
+  int16_t pad0;                 // (MSCCL_AMD_XCD_ROTATE placement experiment; 0 = identity)
   const char* images;           // thread-block images, tbStride bytes each
   int32_t tbStride;
   int32_t connSplit;            // connection record of (tb, sub): send / recv [tb * connSplit + sub]

@@ -1381,7 +1381,9 @@ __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> 
   const RankWork& w = args.w[r];
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
-  it.runSmall(w, b - w.blockBase);
+  int local = b - w.blockBase;
+  if (w.rotate != 0) local = (local + w.rotate) % w.nBlocks;
+  it.runSmall(w, local);
 }
 
 }  // namespace msccl

@@ -325,11 +325,12 @@ bool smallEligible(const Planned& p, const RankWork& w) {
   const int64_t k = cs > 0 ? sp / cs : 0, m = std::min<int64_t>(std::max<int>(1, w.merge), std::max<int64_t>(1, k));
   const bool onePass = sp <= cs || (cs > 0 && sp % cs == 0 && k % m == 0);
   const bool flat = p.plan.ringColl == kTreeFlat;
+  if (!comm->knobs.smallKernel || !(p.plan.ringColl == 0 || flat) || p.plan.proto != kProtoLL || p.op.devOp > 3 ||
+      !onePass || !(w.trace == nullptr || comm->traceLight) || w.npkit != nullptr || (w.split & (w.split - 1)) != 0)
+    return false;
+  // (ring / tree plans have no algorithm: algoIndex -1 is only read past the checks above)
   const int64_t chunks = flat ? comm->nRanks : maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop);
-  return comm->knobs.smallKernel && (p.plan.ringColl == 0 || flat) && p.plan.proto == kProtoLL &&
-         p.op.devOp <= 3 && onePass && (w.trace == nullptr || comm->traceLight) && w.npkit == nullptr &&
-         (w.split & (w.split - 1)) == 0 &&
-         p.plan.sizePerChunk * chunks * refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit offsets
+  return p.plan.sizePerChunk * chunks * refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit offsets
 }
 
 ncclResult_t launchGroup(std::vector<Planned*>& ps) {
@@ -349,6 +350,14 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   }
   args.nRanks = (int)ps.size();
   if (blocks == 0) return ncclSuccess;
+  {
+    // MSCCL_AMD_XCD_ROTATE=K: co-resident rank i's workgroups run slots shifted by i * K (a
+    // placement experiment: workgroups are dealt to XCDs by grid index; the small kernel only)
+    static const int64_t rot = envInt("MSCCL_AMD_XCD_ROTATE", 0);
+    if (rot != 0)
+      for (size_t i = 0; i < ps.size(); i++)
+        if (args.w[i].nBlocks > 0) args.w[i].rotate = (int16_t)((rot * (int64_t)i) % args.w[i].nBlocks);
+  }
   EventPool& pool = tEvents[dev];
   pool.used = 0;
   for (size_t i = 1; i < ps.size(); i++) {
