@@ -279,7 +279,9 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         xmls = {"ar": xmlgen.allreduce_ring(n, chans, "Simple", True, 0, 1 << 40, name="c4_ring")}
         dt, S = M.BFLOAT16, 256 << 20
     elif cfg == "C5":
-        c5i = int(os.environ.get("MSCCL_AMD_BENCH_C5_INSTANCES", "0")) or 16  # 2 ranks: RS 126 -> 243, AG 225 -> 373 GB/s vs 4
+        # 2 ranks: 16 instances (RS 126 -> 243, AG 225 -> 373 GB/s against 4); more ranks: 4, so
+        # n (n-1) x instances thread blocks stay resident when the ranks share one GPU
+        c5i = int(os.environ.get("MSCCL_AMD_BENCH_C5_INSTANCES", "0")) or (16 if n <= 2 else 4)
         xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_rs"),
                 "ag": xmlgen.allgather_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_ag")}
         dt, S = M.FLOAT32, 64 << 20
@@ -295,6 +297,16 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         open(pth, "w").write(x)
         paths.append(pth)
     os.environ["MSCCL_XML_FILES"] = ":".join(paths)
+    # algorithmic HBM bytes of one launch on this GPU, summed over the ranks it runs (schedule_bytes)
+    ranks_here = [rank] if multi else list(range(n))
+
+    def launch_bytes(path, coll_count, mult, ts_):
+        tot = 0
+        for r in ranks_here:
+            al = M.algo_json(path, r, n)
+            size_per = coll_count * mult // al["nchunksperloop"]
+            tot += schedule_bytes(al, size_per, ts_, al["proto"])[0]
+        return tot
 
     def note(msg):
         if rank == 0 and not a.quiet:
@@ -337,7 +349,7 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 step()
                 torch.cuda.synchronize()
                 return agree(all(torch.equal(b.view(torch.uint8)[:S].view(tdt), want) for b in bufs))
-            phases = {"allreduce": (step, S * 2 * (n - 1) / n)}
+            phases = {"allreduce": (step, S * 2 * (n - 1) / n, launch_bytes(paths[0], cnt, 1, ts))}
         else:
             rc = S // ts // n
             ins = [torch.empty(S // 4, dtype=torch.float32, device=dev).uniform_(-1, 1) for _ in range(nloc)]
@@ -364,10 +376,11 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 torch.cuda.synchronize()
                 good = all(torch.equal(m, full[r * rc:(r + 1) * rc]) for r, m in zip(ranks, mids))
                 return agree(good and all(torch.equal(o, full) for o in outs))
-            phases = {"reduce_scatter": (rs, S * (n - 1) / n), "all_gather": (ag, S * (n - 1) / n)}
+            phases = {"reduce_scatter": (rs, S * (n - 1) / n, launch_bytes(paths[0], rc, n, ts)),
+                      "all_gather": (ag, S * (n - 1) / n, launch_bytes(paths[1], rc * ts, n, 1))}
         res = {}
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for name, (fn, busbytes) in phases.items():
+        for name, (fn, busbytes, algo_bytes) in phases.items():
             note("%s warmup" % name)
             for _ in range(max(1, a.warmup)):
                 fn()
@@ -392,7 +405,10 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
             if any(c.async_error() != 0 for c in comms):
                 raise RuntimeError("kernel reported an error (timeout/abort)")
             res[name] = {"ms": round(t * 1e3, 4), "kernel_ms": round(ev_ms, 4),
-                         "busbw": round(busbytes / t / 1e9, 3), "steps": k}
+                         "busbw": round(busbytes / t / 1e9, 3), "steps": k,
+                         # roofline: algorithmic HBM bytes of the launch on this GPU / its event time
+                         "algorithmic_bytes_per_launch": algo_bytes,
+                         "hbm_frac": round(algo_bytes / (ev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}
             note("%s %.3f ms, busbw %.1f GB/s" % (name, t * 1e3, busbytes / t / 1e9))
         res["verified"] = check()
         res["bytes"] = S
@@ -663,10 +679,10 @@ def main():
     # Clock warm-up before the sweep: an idle GPU starts the first timed size at low clocks (the
     # 128 B point once read 27 us instead of 8-9 us).  One process: about 0.3 s of mid-size
     # AllReduces.  Several: every rank must issue the same number of collectives, so a fixed count.
-    # (A one-size run, e.g. a rocprofv3 pass over the headline, skips it: its warmup steps warm the
-    # clocks, and every interpreter dispatch of the run is then a launch of that size.)
-    wsize = min(maxb, 1 << 20)
-    if len(sizes) > 1 and (wsize // ts) % algos[tier_of(tiers, wsize)[3]]["nchunksperloop"] == 0:
+    # A one-size run (a rocprofv3 pass over the headline) warms up with that size, so every
+    # interpreter dispatch of the run is a launch of that size.
+    wsize = maxb if len(sizes) == 1 else min(maxb, 1 << 20)
+    if (wsize // ts) % algos[tier_of(tiers, wsize)[3]]["nchunksperloop"] == 0:
         if multi:
             for _ in range(1000):
                 one_step(wsize)

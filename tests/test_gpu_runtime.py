@@ -142,7 +142,8 @@ def test_no_match_falls_back_to_ring(tmp_path):
                 assert torch.equal(b.cpu(), x[0] + x[1]), (count, inplace)
         assert all(c.async_error() == 0 for c in comms)
         # 4 all-pairs channels + 32 ring channels + 32 tree channels (rank 0 is the chain's root)
-        assert comms[0].info()["sendConns"] == 4 + 32 + 32
+        # + the flat tree's connection to every peer (transport.cc: flatPeers)
+        assert comms[0].info()["sendConns"] == 4 + 32 + 32 + 1
     finally:
         for c in comms:
             c.destroy()

@@ -52,6 +52,36 @@ def counter_avg(d, counter):
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
+def per_kernel(out):
+    """Every interpreter kernel of the run separately (a run timing several configurations
+    launches a different kernel instantiation per configuration): calls, average duration from
+    the trace, FETCH_SIZE / WRITE_SIZE averages and the traffic they imply."""
+    res = {}
+    for f in find(os.path.join(out, "kt"), "*kernel_trace.csv"):
+        for r in rows(f):
+            name = col(r, "Kernel_Name", "KernelName")
+            if is_msccl(name):
+                d = res.setdefault(name, {"durs": []})
+                d["durs"].append(int(col(r, "End_Timestamp", "EndNs")) - int(col(r, "Start_Timestamp", "BeginNs")))
+    for sub, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
+        for f in find(os.path.join(out, sub), "*counter_collection.csv"):
+            for r in rows(f):
+                name = col(r, "Kernel_Name", "KernelName", "Kernel-Name")
+                if is_msccl(name) and col(r, "Counter_Name", "CounterName") == counter:
+                    res.setdefault(name, {"durs": []}).setdefault(counter, []).append(
+                        float(col(r, "Counter_Value", "CounterValue")))
+    out_d = {}
+    for name, d in res.items():
+        e = {"launches": len(d["durs"]), "avg_ns": sum(d["durs"]) / len(d["durs"]) if d["durs"] else None}
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            v = d.get(counter, [])
+            e[counter.lower() + "_kib_avg"] = sum(v) / len(v) if v else None
+        if e["fetch_size_kib_avg"] is not None and e["write_size_kib_avg"] is not None:
+            e["traffic_bytes_per_launch"] = (2.0 * e["fetch_size_kib_avg"] + e["write_size_kib_avg"]) * 1024.0
+        out_d[name] = e
+    return out_d
+
+
 def main():
     out, tag = sys.argv[1], sys.argv[2]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -87,6 +117,7 @@ def main():
     if fetch is not None and write is not None:
         res["traffic_bytes_per_launch"] = (2.0 * fetch + write) * 1024.0
         res["traffic_note"] = "(2 x FETCH_SIZE + WRITE_SIZE) x 1024 per interpreter-kernel dispatch (gfx950 FETCH_SIZE correction)"
+    res["per_kernel"] = per_kernel(out)
     kt = os.path.join(out, "kt.json")
     if os.path.exists(kt):
         try:
