@@ -282,7 +282,8 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         # 2 ranks: 16 instances (RS 126 -> 243, AG 225 -> 373 GB/s against 4); more ranks: 4, so
         # n (n-1) x instances thread blocks stay resident when the ranks share one GPU
         c5i = int(os.environ.get("MSCCL_AMD_BENCH_C5_INSTANCES", "0")) or (16 if n <= 2 else 4)
-        xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_rs"),
+        rs_form = os.environ.get("MSCCL_AMD_BENCH_RS_FORM", "chain")   # "scratch": the round-2 form
+        xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_rs", form=rs_form),
                 "ag": xmlgen.allgather_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_ag")}
         dt, S = M.FLOAT32, 64 << 20
     elif cfg == "FB":
@@ -415,7 +416,8 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         res["dtype"] = {M.BFLOAT16: "bf16", M.FLOAT32: "f32"}[dt]
         res["ranks"] = n
         res["schedule"] = {"C4": "allreduce_ring x%d Simple" % chans if cfg == "C4" else "",
-                           "C5": "reduce_scatter_allpairs + allgather_allpairs x%d Simple" % c5i if cfg == "C5" else "",
+                           "C5": "reduce_scatter_allpairs (%s) + allgather_allpairs x%d Simple" % (rs_form, c5i)
+                                 if cfg == "C5" else "",
                            "FB": "ring fallback (no schedule matches)"}[cfg]
         return res
     finally:

@@ -14,7 +14,8 @@ import os
 from typing import List, Optional, Sequence
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmsccl_amd.so")
+# MSCCL_AMD_LIB points at another build of the library (A/B measurements of two builds on one box)
+LIB_PATH = os.environ.get("MSCCL_AMD_LIB") or os.path.join(_HERE, "libmsccl_amd.so")
 
 # trace event layout (include/msccl_amd.h: mscclAmdTraceRead); types: 1 setup, 2 dep-wait done,
 # 3 primitive begin (arg = transfer type << 24 | elements), 4 primitive end, 5 end, 0xFFFF header

@@ -107,7 +107,8 @@ struct DevSendConn {
   uint64_t headSeen;            // last head value read: credit known without a poll while step < headSeen + 8
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
-  int32_t remote;               // receiver on another GPU: system-scope release before a tail post
+  int32_t remote;               // 1: receiver on another GPU (system-scope release before a tail post);
+                                // 2: local, agent fences (MSCCL_AMD_SIMPLE_FENCE); 0: local, sc0 sc1 form
   int32_t pad;
 };
 
@@ -120,7 +121,8 @@ struct DevRecvConn {
   uint64_t tailSeen;            // last Simple tail value read (data known present below it)
   int32_t llSlotLines;
   int32_t simpleSlotBytes;
-  int32_t remote;               // sender on another GPU: system-scope acquire after a tail is seen
+  int32_t remote;               // 1: sender on another GPU (system-scope acquire after a tail is seen);
+                                // 2: local, agent fences (MSCCL_AMD_SIMPLE_FENCE); 0: local, sc0 sc1 form
   int32_t pad;
 };
 static_assert(sizeof(DevSendConn) == 64 && sizeof(DevRecvConn) == 64, "connection records are four 16-B units");

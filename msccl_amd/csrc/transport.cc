@@ -205,6 +205,9 @@ static ncclResult_t buildConns(ncclComm* comm, int group, int nTb, const std::ve
                                const std::vector<int>& peerRemote, DevSendConn** dS, DevRecvConn** dR) {
   const int n = comm->nRanks, me = comm->rank, S = groupSubs(comm, group);
   const uint8_t m = groupProtoMask(comm, group);
+  // MSCCL_AMD_SIMPLE_FENCE=1: agent-scope fences around local Simple hand-offs too (a measurement
+  // of what the fences would cost; the sc0 sc1 form needs none, interpreter.h: waitRecvTail)
+  static const int localFence = envInt("MSCCL_AMD_SIMPLE_FENCE", 0) ? 2 : 0;
   const bool needLL = m & ((1u << kProtoLL) | (1u << kProtoLL128)), needS = m & (1u << kProtoSimple);
   std::vector<DevSendConn> hs((size_t)std::max(nTb, 1) * S);
   std::vector<DevRecvConn> hr((size_t)std::max(nTb, 1) * S);
@@ -228,7 +231,7 @@ static ncclResult_t buildConns(ncclComm* comm, int group, int nTb, const std::ve
         c.head = (uint64_t*)(comm->arena + mine.sendHead + s * mine.wordStride);
         c.llSlotLines = comm->llSlotLines;
         c.simpleSlotBytes = comm->simpleSlotBytes;
-        c.remote = peerRemote[p];
+        c.remote = peerRemote[p] ? 1 : localFence;
       }
     }
     if (recvPeer[b] >= 0) {
@@ -248,7 +251,7 @@ static ncclResult_t buildConns(ncclComm* comm, int group, int nTb, const std::ve
         c.remoteHead = (uint64_t*)(peerBases[p] + theirs.sendHead + s * theirs.wordStride);
         c.llSlotLines = comm->llSlotLines;
         c.simpleSlotBytes = comm->simpleSlotBytes;
-        c.remote = peerRemote[p];
+        c.remote = peerRemote[p] ? 1 : localFence;
       }
     }
   }

@@ -14,4 +14,4 @@ mkdir -p $OUT
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py $ARGS > $OUT/kt.json || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- python3 bench.py $ARGS > $OUT/fetch.json || exit 1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $ARGS > $OUT/write.json || exit 1
-python3 tools/parse_prof.py $OUT $TAG
+python3 tools/parse_prof.py $OUT $TAG && cp profiles/${TAG}_* $OUT/   # profiles/ is not copied back from a GPU box
