@@ -61,6 +61,12 @@ int mscclAmdTraceRead(ncclComm_t comm, void* out, size_t outBytes, int* slots, i
 int mscclAmdLineTearProbe(int writerDev, int readerDev, int nLines, int iters, double seconds,
                           unsigned long long* out);
 
+/* Read one NAME=VALUE parameter file into the environment without overwriting variables that are
+ * already set: the reference's setEnvFile (misc/param.cc:25-49), which its initEnv applies to
+ * ~/.nccl.conf and then /etc/nccl.conf before the first parameter read (this library does the
+ * same on its first entry).  Returns 0, or ncclSystemError when the file cannot be opened. */
+int mscclAmdSetEnvFile(const char* path);
+
 #ifdef __cplusplus
 }
 #endif

@@ -5,10 +5,12 @@
 #include <stdlib.h>
 #include <string.h>
 #include <strings.h>
+#include <pwd.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <mutex>
 
 namespace msccl {
@@ -22,7 +24,10 @@ std::mutex gMu;
 thread_local char gLast[1024] = "";
 char gHost[64] = "";
 
+std::once_flag gEnvOnce;
+
 void initLog() {
+  initEnv();
   const char* lvl = getenv("NCCL_DEBUG");
   if (lvl) {
     if (!strcasecmp(lvl, "VERSION")) gLevel = kLogVersion;
@@ -68,7 +73,41 @@ void initLog() {
 
 const char* lastError() { return gLast; }
 
+// The reference's setEnvFile (misc/param.cc:25-49): one NAME=VALUE per line, split at the first
+// '=', a line without '=' skipped, names and values cut at 1023 characters, and an existing
+// environment variable never overwritten (setenv(..., 0)).
+bool setEnvFile(const char* fileName) {
+  FILE* f = fopen(fileName, "r");
+  if (f == nullptr) return false;
+  char* line = nullptr;
+  size_t cap = 0;
+  ssize_t len;
+  while ((len = getline(&line, &cap, f)) != -1) {
+    if (len > 0 && line[len - 1] == '\n') line[--len] = '\0';
+    const char* eq = strchr(line, '=');
+    if (eq == nullptr) continue;
+    std::string name(line, std::min<size_t>(eq - line, 1023));
+    std::string value(eq + 1, std::min<size_t>(strlen(eq + 1), 1023));
+    setenv(name.c_str(), value.c_str(), 0);
+  }
+  free(line);
+  fclose(f);
+  return true;
+}
+
+// initEnv (misc/param.cc:51-60), once per process before the first parameter is read:
+// ~/.nccl.conf (the passwd entry's home, not $HOME), then /etc/nccl.conf.  The environment wins
+// over both, the user's file over the system one.
+void initEnv() {
+  std::call_once(gEnvOnce, [] {
+    const struct passwd* pw = getpwuid(getuid());
+    if (pw != nullptr && pw->pw_dir != nullptr) setEnvFile((std::string(pw->pw_dir) + "/.nccl.conf").c_str());
+    setEnvFile("/etc/nccl.conf");
+  });
+}
+
 int64_t envInt(const char* name, int64_t def) {
+  initEnv();
   const char* v = getenv(name);
   if (!v || !*v) return def;
   char* end = nullptr;

@@ -17,6 +17,11 @@ void logMessage(int level, uint64_t subsys, const char* file, int line, const ch
     __attribute__((format(printf, 5, 6)));
 // Last WARN text (ncclGetLastError, init.cc:1252-1255)
 const char* lastError();
+// ~/.nccl.conf and /etc/nccl.conf into the environment, once (misc/param.cc:51-60); every
+// parameter read below runs it first.
+void initEnv();
+// One NAME=VALUE file into the environment without overwriting (misc/param.cc:25-49).
+bool setEnvFile(const char* fileName);
 // Integer environment parameter (NCCL_PARAM style, param.h:99-108), base prefix accepted.
 int64_t envInt(const char* name, int64_t def);
 

@@ -138,6 +138,11 @@ int mscclAmdBootstrapAllgather(const ncclUniqueId* id, int rank, int nranks, con
   return r;
 }
 
+int mscclAmdSetEnvFile(const char* path) {
+  if (path == nullptr) return ncclInvalidArgument;
+  return setEnvFile(path) ? ncclSuccess : ncclSystemError;
+}
+
 int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex) {
   if (!commValid(comm) || algoIndex < 0 || algoIndex >= (int)comm->algos.size()) return -1;
   return comm->algos[algoIndex].nBlocks;

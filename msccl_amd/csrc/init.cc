@@ -375,11 +375,13 @@ ncclResult_t ncclGetVersion(int* version) {
 }
 
 ncclResult_t ncclGetUniqueId(ncclUniqueId* out) {
+  initEnv();  // ncclInit -> initEnv (init.cc:70-85, misc/param.cc:51-60)
   if (!out) { WARN("ncclGetUniqueId : uniqueId argument is NULL"); return ncclInvalidArgument; }
   return bootstrapCreateRoot(out);
 }
 
 ncclResult_t ncclCommInitRank(ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
+  initEnv();
   if (!newcomm) { WARN("ncclCommInitRank : comm argument is NULL"); return ncclInvalidArgument; }
   if (nranks < 1 || myrank < 0 || myrank >= nranks) {
     WARN("Invalid rank requested : %d/%d", myrank, nranks);
@@ -408,6 +410,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* newcomm, int nranks, ncclUniqueId comm
 // Single process, ndev ranks (init.cc:1099-1117).  devlist may repeat a device: such ranks are
 // co-resident on one GPU and a group of their calls becomes one fused launch.
 ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
+  initEnv();
   if (!comms) { WARN("ncclCommInitAll : comms argument is NULL"); return ncclInvalidArgument; }
   if (ndev < 1) { WARN("ncclCommInitAll : invalid ndev %d", ndev); return ncclInvalidArgument; }
   int ndevices = 0;

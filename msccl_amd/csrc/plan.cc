@@ -52,6 +52,7 @@ static int getNthreads(const char* env) {  // NCCL_PARAM-style cached read; -2 =
 }
 
 Knobs Knobs::fromEnv() {
+  initEnv();  // ~/.nccl.conf, /etc/nccl.conf (the reference's initEnv, before any NCCL_PARAM read)
   Knobs k;
   memset(&k, 0, sizeof(k));
   // The reference runs an MSCCL AllReduce only when NCCL_ALGO lists MSCCL (algoEnable default 0,
