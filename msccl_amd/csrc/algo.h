@@ -44,7 +44,11 @@ enum OpType : uint8_t {
   kSendRecvReduceCopy = 10,
   // `s` fused with the `cpy` of the same source chunks that follows it: one pass that sends the
   // source and copies it (the ring's copy-send); never from XML
-  kSendCopy = 11
+  kSendCopy = 11,
+  // the flat tree's fold (transport.cc: ringUpload): receive every peer's input over the recv
+  // connections of thread blocks 1..n-1 and fold all n inputs, in the order of the reduction
+  // table (thread block per position, -1 = this rank's input), into the output; never from XML
+  kFoldRecv = 12
 };
 
 // Device reduction ops (ncclDevRedOp_t, devcomm.h): Sum, Prod, Max, Min, PreMulSum, SumPostDiv

@@ -92,8 +92,6 @@ struct ncclComm {
   msccl::DevRecvConn* treeRecv = nullptr;
   msccl::DevSendConn* flatSend = nullptr;              // flat tree connections [nRanks] (tb 0 has none)
   msccl::DevRecvConn* flatRecv = nullptr;
-  void* flatScratch = nullptr;                         // flat tree: nRanks slots of a call's bytes
-  size_t flatScratchBytes = 0;
   int llSlotLines = 0, simpleSlotBytes = 0;
   int buffSizes[3] = {0, 0, 0};
 
@@ -169,6 +167,7 @@ int algoSendRunOf(const Algorithm& a);
 std::vector<FuseCandidate> fusableTbs(const Algorithm& a);
 bool sendCopyFusable(const Algorithm& a, const std::vector<Transfer>& ts, size_t i);
 ncclResult_t ringUpload(ncclComm* comm);
+bool flatEnabled(const ncclComm* comm);  // the flat tree's connections and program exist
 
 // enqueue.cc
 int typeSize(ncclDataType_t t);

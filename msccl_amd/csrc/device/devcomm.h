@@ -35,6 +35,7 @@ constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag
 constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
 constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kMaxSplit
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
+constexpr int kMaxFoldPeers = 15;      // flat tree fold: peers of one rank (MSCCL_MAX_REDUCE_FUSION 16 ranks)
 
 // Device trace event (mscclAmdTraceRead).
 struct TraceEvent {
@@ -194,6 +195,7 @@ struct RankWork {
   uint8_t maxAllowedCount;
   uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
   uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
+  uint8_t foldPeers;            // flat tree (mscclFoldKernel): peers, on the records of thread blocks 1..foldPeers
   int64_t maxOpElems;           // largest run of sends before a receive (elements, all sub-connections)
   // ring fallback (kRingNone for MSCCL schedules): the program's offsets are chunk / rank indices
   // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)
@@ -233,6 +235,7 @@ OneRankFn getOneRankFn(int dtype);
 constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = resident workgroups per CU
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
 LaunchFn getSmallLaunchFn(int dtype, int redop);  // mscclSmallKernel (LL, Sum..Min), or null
+LaunchFn getFoldLaunchFn(int dtype, int redop);   // mscclFoldKernel (the flat tree), or null
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):
 // NPKit's host/GPU clock calibration.  Returns 0 on a successful launch.
 int launchClockProbe(uint64_t* hostWord, void* stream);

@@ -43,6 +43,18 @@ struct alignas(16) BlockShared {
   uint32_t aborted;
 };
 
+// The flat tree's fold kernel (Interp::runFold), besides BlockShared: per peer, its send and recv
+// connection records and this step's FIFO slots.
+struct alignas(16) FoldShared {
+  DevSendConn foldSend[kMaxFoldPeers];
+  DevRecvConn foldRecv[kMaxFoldPeers];
+  struct Peer {
+    LLLine* out;        // send slot of this step (peer memory)
+    const LLLine* in;   // recv slot of this step
+    uint32_t sflag, rflag;
+  } fold[kMaxFoldPeers];
+};
+
 __device__ __forceinline__ uint64_t computeFlag(uint64_t workIndex, uint64_t iter, uint64_t step) {
   return workIndex * (65536ull * 256ull) + iter * 256ull + step;  // msccl_interpreter.h:14-16
 }
@@ -1258,6 +1270,186 @@ struct Interp {
     }
   }
 
+  // ---------------------------------------------------------------- the flat tree (mscclFoldKernel)
+  // The flat tree's one-hop AllReduce (transport.cc: ringUpload, plan.cc: makeFlatTreePlan), one
+  // workgroup per rank.  Per FIFO step every lane takes its 16-B packs of the input, stores each
+  // as two LL lines into every peer's slot (the send), then polls the same lines of every peer's
+  // slot here and folds the n inputs in the order of thread block 0's reduction table: acc = x_0,
+  // acc = fn(acc, x_i), the table listing ranks n-1 down to 0, i.e. the chain tree's x_{n-1} (+)
+  // ... (+) x_0, its own input taken from registers at its position, and stores the result.  A
+  // lane reads its input before it writes the output, so in-place calls are safe.  Connections
+  // are the flat group's all-pairs connections, peer k on the records of thread block k + 1
+  // (transport.cc: flatPeers); 8 peers' lines are polled per wait (VGPR addresses only: see
+  // primitives.h ldLines16 on SGPR operands in asm).  No scratch, no flag, no second hop.  Its own kernel: the interpreter
+  // kernels keep their register budget.
+  __device__ __forceinline__ void runFold(const RankWork& w, FoldShared* fs) {
+    tid = threadIdx.x;
+    comm = w.comm;
+    timeoutTicks = w.timeoutTicks;
+    llFlagMask = w.llFlagMask;
+    llCleanMask = w.llCleanMask;
+    redArg = 0;
+    trace = nullptr;
+    nkBuf = nullptr;
+    scG = nullptr;
+    rcG = nullptr;
+    const int np = w.foldPeers;
+    // one round trip: thread block 0's image (the fold order), every peer's send and recv
+    // records, the launch epoch
+    {
+      const u32x4* gimg = (const u32x4*)w.images;
+      const int nU = w.tbStride >> 4;
+      for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
+      if (tid >= 64 && tid < 64 + 4 * np) {
+        const int k = (tid - 64) >> 2, j = (tid - 64) & 3;
+        ((u32x4*)&fs->foldSend[k])[j] = ((const u32x4*)(w.send + (size_t)(k + 1) * w.connSplit))[j];
+      }
+      if (tid >= 192 && tid < 192 + 4 * np) {
+        const int k = (tid - 192) >> 2, j = (tid - 192) & 3;
+        ((u32x4*)&fs->foldRecv[k])[j] = ((const u32x4*)(w.recv + (size_t)(k + 1) * w.connSplit))[j];
+      }
+      if (tid == 128) {
+        sh->aborted = 0;
+        sh->epoch = atomicLoadAgent(w.epochs);
+      }
+    }
+    __syncthreads();
+    const uint64_t workIndex = uni(sh->epoch);
+    DevTbHeader hd;
+    {
+      u32x4 raw = sh->img[0];
+      raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
+      __builtin_memcpy(&hd, &raw, sizeof(hd));
+    }
+    const DevTransfer t = loadTransfer((const DevTransfer*)&sh->img[1]);
+    const int16_t* order = (const int16_t*)((const DevTransfer*)&sh->img[1] + hd.nsteps) + 2 * hd.ndeps + t.redPtr;
+    const int nfold = t.numReds;
+    int ownAt = 0, nq = 0;  // peers folded before the own input
+    for (int i = 0; i < nfold; i++) {
+      if (uni((int)order[i]) < 0) ownAt = nq;
+      else nq++;
+    }
+    constexpr int E = 8 / TS;
+    constexpr int G = 8;  // peers per wait
+    const int n = (int)w.sizePerChunk;
+    const int npk = (n + PE - 1) / PE;
+    const int nlinesFull = (n + E - 1) / E;
+    const __amdgpu_buffer_rsrc_t srs = makeRsrc(w.sendbuff), drs = makeRsrc(w.recvbuff);
+    const bool vec = aligned16(w.sendbuff) && aligned16(w.recvbuff);
+    const int slotLines = uni(fs->foldRecv[0].llSlotLines);
+    const int slotPacks = slotLines / 2;
+    int s0 = 0;
+    do {
+      const int s1 = npk - s0 < slotPacks ? npk : s0 + slotPacks;
+      if (tid < np) {
+        // lane k: peer k's send credit (llOp's waitSendCredit) and both slots of this step
+        DevSendConn& c = fs->foldSend[tid];
+        const uint64_t st = c.step;
+        if (c.headSeen + kLLFifoSlots < st + 1) {
+          Spin spins;
+          uint64_t h;
+          while ((h = atomicLoadSys(c.head)) + kLLFifoSlots < st + 1)
+            if (spinAbort(spins)) break;
+          c.headSeen = h;
+        }
+        fs->fold[tid].out = c.ll + (st % kLLFifoSlots) * (uint64_t)c.llSlotLines;
+        fs->fold[tid].sflag = (uint32_t)(st + 1) & llFlagMask;
+        const DevRecvConn& r = fs->foldRecv[tid];
+        fs->fold[tid].in = r.ll + (r.step % kLLFifoSlots) * (uint64_t)slotLines;
+        fs->fold[tid].rflag = (uint32_t)(r.step + 1) & llFlagMask;
+      }
+      __syncthreads();
+      for (int q = tid; q < s1 - s0; q += kNT) {
+        const int B = s0 + q;
+        const bool two = 2 * B + 1 < nlinesFull;
+        const u32x4 own = loadPack(srs, vec, B, n);
+        const uint32_t o0 = (uint32_t)llLineIdx(q, 0) * 16;
+        const uint32_t o1 = two ? (uint32_t)llLineIdx(q, 1) * 16 : o0;
+        for (int k = 0; k < np; k++) {  // the send: this pack to every peer
+          const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[k].out);
+          const uint32_t f = fs->fold[k].sflag;
+          st16<kAuxFifo>(frs, o0, (u32x4){own.x, f, own.y, f});
+          if (two) st16<kAuxFifo>(frs, o1, (u32x4){own.z, f, own.w, f});
+        }
+        u32x4 acc = (u32x4){0, 0, 0, 0};
+        bool first = true;
+        for (int g0 = 0; g0 < nq; g0 += G) {  // the fold, peers in fold order
+          const void* la[2 * G];
+          int pk[G];
+#pragma unroll
+          for (int k = 0; k < G; k++) {
+            pk[k] = foldPeer(order, nfold, g0 + k < nq ? g0 + k : g0);
+            const char* in = (const char*)fs->fold[pk[k]].in;
+            la[2 * k] = in + o0;
+            la[2 * k + 1] = in + o1;
+          }
+          u32x4 ln[2 * G];
+          ldLines16(la, ln);
+#pragma unroll
+          for (int k = 0; k < G; k++) {
+            const int p = g0 + k;
+            if (p >= nq) continue;
+            if (p == ownAt) {
+              acc = first ? own : F::pack(acc, own);
+              first = false;
+            }
+            const uint32_t rflag = fs->fold[pk[k]].rflag;
+            Spin spins;
+            while (ln[2 * k].y != rflag || ln[2 * k].w != rflag || ln[2 * k + 1].y != rflag ||
+                   ln[2 * k + 1].w != rflag) {
+              if (spinAbort(spins)) break;
+              ldLines2(la[2 * k], la[2 * k + 1], ln[2 * k], ln[2 * k + 1]);
+            }
+            const u32x4 peer = {ln[2 * k].x, ln[2 * k].z, ln[2 * k + 1].x, ln[2 * k + 1].z};
+            acc = first ? peer : F::pack(acc, peer);
+            first = false;
+          }
+        }
+        if (ownAt == nq) acc = first ? own : F::pack(acc, own);
+        storePack(drs, vec, B, n, acc);
+      }
+      for (int k = 0; k < np; k++) {
+        // LL cleanup (prims_ll.h:90-97): on cleanup steps stamp the send slot's unused lines
+        const uint64_t st = uni(fs->foldSend[k].step);
+        if ((st & llCleanMask) != llCleanMask) continue;
+        const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[k].out);
+        const uint32_t f = fs->fold[k].sflag;
+        for (int l = tid; l < slotLines; l += kNT) {
+          const int q = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
+          const bool used = s0 + q < s1 && 2 * (s0 + q) + h < nlinesFull;
+          if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, f, 0, f});
+        }
+      }
+      __syncthreads();
+      if (tid < np) {  // this step's slots are consumed / filled: free the peer's slot (head post)
+        fs->foldSend[tid].step++;
+        const uint64_t rs = fs->foldRecv[tid].step + 1;
+        fs->foldRecv[tid].step = rs;
+        atomicStoreSys(fs->foldRecv[tid].remoteHead, rs);
+      }
+      s0 = s1;
+    } while (s0 < npk);
+    __syncthreads();
+    if (tid < np) {  // persist the connections' steps (flat records of thread block k + 1)
+      DevSendConn* cg = w.send + (size_t)(tid + 1) * w.connSplit;
+      cg->step = fs->foldSend[tid].step;
+      cg->headSeen = fs->foldSend[tid].headSeen;
+      (w.recv + (size_t)(tid + 1) * w.connSplit)->step = fs->foldRecv[tid].step;
+    }
+    epilogue(w, 0, 0, workIndex);
+  }
+  // index of the p-th peer in fold order (order: thread block per fold position, -1 = own input)
+  static __device__ __forceinline__ int foldPeer(const int16_t* order, int nfold, int p) {
+    int j = 0, k = 0;
+    for (int i = 0; i < nfold; i++) {
+      const int b = order[i];
+      if (b < 0) continue;
+      if (j == p) k = b - 1;
+      j++;
+    }
+    return k;
+  }
+
   // ---------------------------------------------------------------- small calls
   // A launch whose every rank's call runs run()'s loop as equal passes: one iteration
   // (sizePerChunk <= chunkSize) or full iterations merged `merge` at a time with nothing left
@@ -1347,13 +1539,17 @@ struct Interp {
         if (!runPass(grid, iter)) break;
     }
     epilogue(w, bid, sub, workIndex);
-    if (w.trace != nullptr && tid == 0) {  // light trace: this workgroup's start and end only
+    if (w.trace != nullptr && tid == 0) {
+      // light trace (MSCCL_AMD_TRACE=2): this workgroup's start, and its end with the XCD it ran on
+      // (HW_REG_XCC_ID: the dispatch order only says which blocks share an XCD, not which one)
+      uint32_t xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
       TraceEvent* tr = w.trace + (size_t)(bid * maxSplit + sub) * w.traceEvents;
       TraceEvent e;
       e.ts = __builtin_amdgcn_s_memrealtime();
       e.type = kEvEnd;
       e.step = 0;
-      e.arg = 0;
+      e.arg = xcc & 0xf;
       tr[1] = e;
       e.ts = tStart;
       e.type = kEvHeader;
@@ -1391,6 +1587,16 @@ __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> 
   int local = b - w.blockBase;
   if (w.rotate != 0) local = (local + w.rotate) % w.nBlocks;
   it.runSmall(w, local);
+}
+
+// The flat tree's fold kernel (Interp::runFold): workgroup r runs rank r of the launch.
+template <typename T, int OP, int R>
+__global__ void __launch_bounds__(kNT, 1) mscclFoldKernel(const LaunchArgsN<R> args) {
+  __shared__ BlockShared sh;
+  __shared__ FoldShared fs;
+  Interp<T, OP, pLL> it;
+  it.sh = &sh;
+  it.runFold(args.w[blockIdx.x], &fs);
 }
 
 }  // namespace msccl

@@ -45,6 +45,30 @@ int launchSmallKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// the flat tree's fold kernel (mscclFoldKernel, LL, Sum..Min): one workgroup per rank
+template <typename T, int OP>
+int launchFoldKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  constexpr int RC = kCompactLaunchRanks;
+  if (gridBlocks == kQueryResidency) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclFoldKernel<T, OP, kMaxLaunchRanks>, kNT, 0) != hipSuccess)
+      return 0;
+    return n;
+  }
+  if (gridBlocks != args.nRanks) return 1;  // one workgroup per rank (RankWork::nBlocks == 1)
+  if (args.nRanks <= RC) {
+    LaunchArgsN<RC> a;
+    a.nRanks = args.nRanks;
+    a.pad = 0;
+    for (int r = 0; r < RC; r++) a.w[r] = args.w[r];
+    hipLaunchKernelGGL((mscclFoldKernel<T, OP, RC>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL((mscclFoldKernel<T, OP, kMaxLaunchRanks>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream,
+                       args);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // nRanks == 1 with a user PreMulSum op: dst = src * scale (the reference's oneRankReduce,
 // onerank_reduce.cu:12-44: ReduceOrCopyMulti with the preOp applied, postOp identity).
 template <typename T>
@@ -78,7 +102,9 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
 // Small-call kernels: MSCCL schedules (ops Sum..Min) on LL.
 #define MSCCL_SMALL(NAME, T)                                                                               \
   LaunchFn NAME##_small[4] = {launchSmallKernel<T, kSum, pLL>, launchSmallKernel<T, kProd, pLL>,          \
-                              launchSmallKernel<T, kMax, pLL>, launchSmallKernel<T, kMin, pLL>};
+                              launchSmallKernel<T, kMax, pLL>, launchSmallKernel<T, kMin, pLL>};          \
+  LaunchFn NAME##_fold[4] = {launchFoldKernel<T, kSum>, launchFoldKernel<T, kProd>, launchFoldKernel<T, kMax>, \
+                             launchFoldKernel<T, kMin>};
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \
                          {launchKernel<T, kSumPostDiv, pLL>, nullptr, launchKernel<T, kSumPostDiv, pSimple>}}; \

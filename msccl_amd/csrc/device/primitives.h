@@ -140,6 +140,35 @@ __device__ __forceinline__ void ldLines8(const void* const* p, u32x4* x) {
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
       : "memory");
 }
+// Sixteen FIFO lines (the flat tree's fold: two lines of 8 peers) in flight, one wait.  Every
+// address is a VGPR pair: no SGPR operand in inline asm, whose "VALU writes SGPR -> VMEM reads it"
+// wait states the compiler's hazard recognizer does not insert for asm (a readfirstlane'd slot
+// base used as a global_ saddr right after it read a stale base and faulted, timing-dependent).
+__device__ __forceinline__ void ldLines16(const void* const* p, u32x4* x) {
+  asm volatile(
+      "global_load_dwordx4 %0, %16, off sc0 sc1\n\t"
+      "global_load_dwordx4 %1, %17, off sc0 sc1\n\t"
+      "global_load_dwordx4 %2, %18, off sc0 sc1\n\t"
+      "global_load_dwordx4 %3, %19, off sc0 sc1\n\t"
+      "global_load_dwordx4 %4, %20, off sc0 sc1\n\t"
+      "global_load_dwordx4 %5, %21, off sc0 sc1\n\t"
+      "global_load_dwordx4 %6, %22, off sc0 sc1\n\t"
+      "global_load_dwordx4 %7, %23, off sc0 sc1\n\t"
+      "global_load_dwordx4 %8, %24, off sc0 sc1\n\t"
+      "global_load_dwordx4 %9, %25, off sc0 sc1\n\t"
+      "global_load_dwordx4 %10, %26, off sc0 sc1\n\t"
+      "global_load_dwordx4 %11, %27, off sc0 sc1\n\t"
+      "global_load_dwordx4 %12, %28, off sc0 sc1\n\t"
+      "global_load_dwordx4 %13, %29, off sc0 sc1\n\t"
+      "global_load_dwordx4 %14, %30, off sc0 sc1\n\t"
+      "global_load_dwordx4 %15, %31, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(x[0]), "=&v"(x[1]), "=&v"(x[2]), "=&v"(x[3]), "=&v"(x[4]), "=&v"(x[5]), "=&v"(x[6]), "=&v"(x[7]),
+        "=&v"(x[8]), "=&v"(x[9]), "=&v"(x[10]), "=&v"(x[11]), "=&v"(x[12]), "=&v"(x[13]), "=&v"(x[14]), "=&v"(x[15])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]),
+        "v"(p[8]), "v"(p[9]), "v"(p[10]), "v"(p[11]), "v"(p[12]), "v"(p[13]), "v"(p[14]), "v"(p[15])
+      : "memory");
+}
 __device__ __forceinline__ void ldLine1(const void* a, u32x4& x) {
   asm volatile(
       "global_load_dwordx4 %0, %1, off sc0 sc1\n\t"

@@ -92,7 +92,7 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
   if (idx < 0) {
     // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
     if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
-      if (comm->flatScratch) makeFlatTreePlan(c, comm->knobs, comm->flatScratchBytes, &out->plan);
+      if (flatEnabled(comm)) makeFlatTreePlan(c, comm->knobs, &out->plan);
       INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; %s fallback (%s, %d channels)",
            op.coll, op.count, (int)op.dtype,
            out->plan.ringColl == kTreeFlat ? "flat tree" : out->plan.ringColl == kTreeAllReduce ? "tree" : "ring",
@@ -127,7 +127,7 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
     // happens when MSCCL_AMD_MAX_SCRATCH capped it.  The reference reports ncclInternalError
     // (enqueue.cc:580-589); the capped schedule is treated as not matching instead.
     if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
-      if (comm->flatScratch) makeFlatTreePlan(c, comm->knobs, comm->flatScratchBytes, &out->plan);
+      if (flatEnabled(comm)) makeFlatTreePlan(c, comm->knobs, &out->plan);
       INFO(kSubColl, "MSCCL: scratch %zu < %zu needed (MSCCL_AMD_MAX_SCRATCH); ring fallback", comm->scratchSize,
            out->plan.scratchNeeded);
       return ncclSuccess;
@@ -193,7 +193,7 @@ RankWork makeFlatWork(Planned& p) {
   memset(&w, 0, sizeof(w));
   w.sendbuff = p.op.sendbuff;
   w.recvbuff = p.op.recvbuff;
-  w.scratch = comm->flatScratch;
+  w.scratch = nullptr;  // the fold reads the FIFOs: no scratch
   w.comm = comm->dComm;
   w.send = da.dSend;
   w.recv = da.dRecv;
@@ -222,6 +222,8 @@ RankWork makeFlatWork(Planned& p) {
     merge = (int)std::max<int64_t>(1, std::min<int64_t>(64, w.maxOpElems / chunk));
   }
   w.merge = (uint8_t)merge;
+  w.nBlocks = 1;  // mscclFoldKernel: one workgroup per rank (interpreter.h: runFold)
+  w.foldPeers = (uint8_t)(comm->nRanks - 1);
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.launchSeq = comm->workIndex++;
@@ -329,7 +331,7 @@ bool smallEligible(const Planned& p, const RankWork& w) {
       !onePass || !(w.trace == nullptr || comm->traceLight) || w.npkit != nullptr || (w.split & (w.split - 1)) != 0)
     return false;
   // (ring / tree plans have no algorithm: algoIndex -1 is only read past the checks above)
-  const int64_t chunks = flat ? comm->nRanks : maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop);
+  const int64_t chunks = flat ? 1 : maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop);
   return p.plan.sizePerChunk * chunks * refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit offsets
 }
 
@@ -368,8 +370,12 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
     }
   }
   const Planned& p0 = *ps[0];
-  LaunchFn fn = small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp) : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
-  for (Planned* p : ps) p->op.comm->last.small = small ? 1 : 0;
+  // a launch group holds flat-tree works only or none (executeOps keys launches on it)
+  const bool fold = p0.plan.ringColl == kTreeFlat;
+  LaunchFn fn = fold ? getFoldLaunchFn(p0.plan.dtype, p0.op.devOp)
+                     : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp)
+                             : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
+  for (Planned* p : ps) p->op.comm->last.small = fold ? 2 : small ? 1 : 0;
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {
     // Every workgroup of the launch may spin on every other one (FIFO credits, dependency
@@ -448,7 +454,7 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
     }
     if (res != ncclSuccess) break;
     // copies / one-rank scaling run at once; kernels are fused per (device, type, op, protocol)
-    typedef std::tuple<int, int, int, int> LaunchKey;
+    typedef std::tuple<int, int, int, int, bool> LaunchKey;  // + flat tree (its own kernel)
     std::vector<std::pair<LaunchKey, std::vector<Planned*>>> launches;
     for (auto& p : planned) {
       if (p.noop) continue;
@@ -468,7 +474,8 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
         }
         continue;
       }
-      const LaunchKey key = std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto);
+      const LaunchKey key =
+          std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto, p.plan.ringColl == kTreeFlat);
       size_t j = 0;
       while (j < launches.size() && launches[j].first != key) j++;
       if (j == launches.size()) launches.emplace_back(key, std::vector<Planned*>());

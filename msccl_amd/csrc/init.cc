@@ -87,16 +87,6 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
     NCCLCHECK(hipErr(hipMemset(comm->scratch, 0, scratch), "hipMemset scratch"));
     comm->scratchSize = scratch;
   }
-  // flat tree (plan.cc: makeFlatTreePlan): n scratch slots of the largest call the tree takes
-  // (MSCCL_AMD_TREE_MAX_BYTES per rank, default 16 KiB x n), at most 256 KiB per slot
-  if (comm->ringFallback && comm->knobs.treeFlat && comm->nRanks > 1 && comm->nRanks <= kMaxReduceFusion) {
-    const int64_t treeMax = comm->knobs.treeMaxBytes >= 0 ? comm->knobs.treeMaxBytes : (int64_t)16384 * comm->nRanks;
-    const size_t slot = (size_t)std::min<int64_t>(std::max<int64_t>(treeMax, 0), 256 << 10);
-    if (slot > 0) {
-      comm->flatScratchBytes = slot * comm->nRanks;
-      NCCLCHECK(hipErr(hipMalloc(&comm->flatScratch, comm->flatScratchBytes), "hipMalloc flat scratch"));
-    }
-  }
   return ncclSuccess;
 }
 
@@ -342,7 +332,6 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
   if (comm->treeRecv) hipFree(comm->treeRecv);
   if (comm->flatSend) hipFree(comm->flatSend);
   if (comm->flatRecv) hipFree(comm->flatRecv);
-  if (comm->flatScratch) hipFree(comm->flatScratch);
   for (size_t r = 0; r < comm->peerArena.size(); r++)
     if (comm->peerArenaIpc[r] && comm->peerArena[r]) hipIpcCloseMemHandle(comm->peerArena[r]);
   if (comm->dComm) hipFree(comm->dComm);

@@ -243,12 +243,13 @@ static int makeTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   return 0;
 }
 
-int makeFlatTreePlan(const CallDesc& c, const Knobs& k, size_t scratchBytes, Plan* p) {
+int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   if (!k.treeFlat || p->ringColl != kTreeAllReduce || p->proto != kProtoLL || c.redop > kDevMin ||
-      c.nRanks < 2 || c.nRanks > kMaxReduceFusion || (size_t)p->nBytes * c.nRanks > scratchBytes)
+      c.nRanks < 2 || c.nRanks > kMaxReduceFusion || p->nBytes > (1ll << 30))
     return 1;
-  // The program (transport.cc: flatProgram) is an MSCCL schedule with one chunk per loop: input
-  // chunk 0, scratch chunks 0..n-1.  Chunk math of makePlan for LL (enqueue.cc:591-734,
+  // It runs in its own kernel (interpreter.h: runFold) as one call over the whole buffer (at
+  // most 1 GiB: 32-bit offsets); the fields below keep the MSCCL plan's form for introspection,
+  // sizePerChunk = count being what the kernel reads.  Chunk math of makePlan for LL (enqueue.cc:591-734,
   // msccl_interpreter.h:79-86) with nchunksPerLoop 1 and the tree's thread count.
   const int ts = refTypeSize(p->dtype);
   const int nt = p->refNthreads;
@@ -262,7 +263,7 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, size_t scratchBytes, Pla
   p->minChunk = std::max<int64_t>(1, (int64_t)nt * (8 / ts));
   p->sizePerChunk = p->count;
   p->nIters = (int)((p->sizePerChunk + p->chunkSize - 1) / p->chunkSize);
-  p->scratchNeeded = (size_t)p->nBytes * c.nRanks;
+  p->scratchNeeded = 0;
   return 0;
 }
 

@@ -94,9 +94,9 @@ int chooseSplit(int maxBlocks, int coResident, const Knobs& k);
 int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p);
 // The flat tree (kTreeFlat): a tree AllReduce plan (makeRingPlan chose the tree, LL, op Sum..Min,
 // 2..16 ranks) turned into a one-iteration-per-chunk MSCCL plan of the flat program
-// (transport.cc: flatProgram): every rank sends its input to every peer's scratch slot and folds
-// the n slots in the chain tree's order x_{n-1} (+) x_{n-2} (+) ... (+) x_0, one hop instead of
-// 2 (n - 1).  Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).
-int makeFlatTreePlan(const CallDesc& c, const Knobs& k, size_t scratchBytes, Plan* p);
+// (transport.cc: ringUpload): every rank sends its input to every peer, and one workgroup folds
+// the n inputs straight from the FIFOs in the chain tree's order x_{n-1} (+) x_{n-2} (+) ... (+)
+// x_0 (interpreter.h: foldRecv), one hop instead of 2 (n - 1).  Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).
+int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p);
 
 }  // namespace msccl

@@ -75,10 +75,11 @@ void flatPeers(int rank, int n, std::vector<int>* sp, std::vector<int>* rp) {
       b++;
     }
 }
+}  // namespace
+
 bool flatEnabled(const ncclComm* comm) {
   return comm->ringFallback && comm->knobs.treeFlat && comm->nRanks > 1 && comm->nRanks <= kMaxReduceFusion;
 }
-}  // namespace
 
 size_t tableIndex(int group, int chan, int peer, int nRanks) {
   return ((size_t)group * kMaxChannels + chan) * nRanks + peer;
@@ -442,68 +443,47 @@ ncclResult_t ringUpload(ncclComm* comm) {
     NCCLCHECK(uploadImages(img, &d));
   }
   if (flatEnabled(comm)) {
-    // The flat tree (plan.cc: makeFlatTreePlan), an MSCCL schedule of one chunk per loop:
-    //   tb 1 + j (peer p_j): s i0 -> p_j (its scratch slot r), r from p_j -> scratch slot p_j;
-    //   tb 0: cpy i0 -> scratch slot r; wait for every peer's r; re into slot n - 1 from slots
-    //   n - 2, ..., 0 (LL order: acc = slot n-1, acc = acc (+) slot q, q descending, skipping
-    //   n - 1); cpy slot n - 1 -> o0.
-    // The fold is the chain tree's (runTreeSplit on the chain, transport.cc: treePeers): leaf
+    // The flat tree (plan.cc: makeFlatTreePlan), run by mscclFoldKernel (interpreter.h: runFold),
+    // one workgroup per rank: it sends its input to every peer p_j over the flat connections of
+    // thread block 1 + j (flatPeers) and folds every rank's input, in the order x_{n-1}, ...,
+    // x_0: acc = x_{n-1}, acc = fn(acc, x_q) for q = n - 2 down to 0.  The order is the one
+    // image uploaded here: thread block 0's reduction table, one entry per rank from n - 1 down
+    // to 0, the thread block whose connections carry that rank (-1: this rank's own input).
+    // That is the chain tree's fold (runTreeSplit on the chain, transport.cc: treePeers): leaf
     // n - 1 sends its input up, rank q folds fn(child's partial, x_q), the root's result comes
     // back down.  Every op admitted (Sum, Prod, Max, Min) is commutative per element, so the
-    // values are the tree's bit for bit, whatever side of fn each operand sits on.
+    // values are the tree's bit for bit, whatever side of fn each operand sits on.  One hop: no
+    // scratch, no dependency flag, no copy.
     const int r = comm->rank;
     std::vector<int> sp, rp;
     flatPeers(r, n, &sp, &rp);
-    auto mk = [](uint8_t type, uint8_t sb, int so, uint8_t db, int dof) {
-      Transfer t;
-      t.type = type;
-      t.srcbuf = sb;
-      t.srcoff = (int16_t)so;
-      t.dstbuf = db;
-      t.dstoff = (int16_t)dof;
-      t.count = 1;
-      return t;
-    };
-    std::vector<Transfer> fold;
-    fold.push_back(mk(kLocalCopy, kInput, 0, kScratch, r));
-    Transfer re = mk(kReduce, kScratch, n - 2, kScratch, n - 1);
-    re.numDeps = (int16_t)(n - 1);
-    re.depPtr = 0;
-    re.numReds = (int16_t)(n - 1);
-    re.redPtr = 0;
-    fold.push_back(re);
-    fold.push_back(mk(kLocalCopy, kScratch, n - 1, kOutput, 0));
-    std::vector<int16_t> depBid, depStep, reds;
-    for (int b = 1; b < n; b++) {
-      depBid.push_back((int16_t)b);
-      depStep.push_back(1);   // the peer thread block's r (its transfer 1) publishes step 1
+    Transfer fold;
+    fold.type = kFoldRecv;
+    fold.srcbuf = kInput;
+    fold.dstbuf = kOutput;
+    fold.count = 1;
+    std::vector<int16_t> order;
+    for (int q = n - 1; q >= 0; q--) {
+      int tb = -1;
+      for (int b = 1; b < n; b++)
+        if (rp[b] == q) tb = b;
+      order.push_back((int16_t)(q == r ? -1 : tb));
     }
-    for (int q = n - 2; q >= 0; q--) reds.push_back((int16_t)q);
+    fold.numReds = (int16_t)order.size();
+    fold.redPtr = 0;
     DevAlgoHost& d = comm->ringAlgos[5];
-    d.nBlocks = n;
-    d.tbStride = (int)std::max(imageBytes(fold.size(), depBid.size(), reds.size()), imageBytes(2, 0, 0));
+    d.nBlocks = 1;
+    d.tbStride = (int)imageBytes(1, 0, order.size());
     d.connSplit = 1;
     d.dSend = comm->flatSend;
     d.dRecv = comm->flatRecv;
-    std::vector<char> img((size_t)d.tbStride * n, 0);
+    std::vector<char> img((size_t)d.tbStride, 0);
+    DevTbHeader h;
+    memset(&h, 0, sizeof(h));
+    h.nsteps = 1;
+    h.nreds = (uint16_t)order.size();
     const std::vector<int16_t> none;
-    for (int b = 0; b < n; b++) {
-      DevTbHeader h;
-      memset(&h, 0, sizeof(h));
-      h.hasSend = sp[b] >= 0;
-      h.hasRecv = rp[b] >= 0;
-      if (b == 0) {
-        h.nsteps = (uint16_t)fold.size();
-        h.ndeps = (uint16_t)depBid.size();
-        h.nreds = (uint16_t)reds.size();
-        putImage(img, 0, h, fold, depBid, depStep, reds);
-      } else {
-        std::vector<Transfer> ex{mk(kSend, kInput, 0, kScratch, r), mk(kRecv, kInput, -1, kScratch, rp[b])};
-        ex[1].hasDep = 1;
-        h.nsteps = 2;
-        putImage(img, (size_t)b * d.tbStride, h, ex, none, none, none);
-      }
-    }
+    putImage(img, 0, h, std::vector<Transfer>{fold}, none, none, order);
     NCCLCHECK(uploadImages(img, &d));
   }
   return ncclSuccess;

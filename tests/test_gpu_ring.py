@@ -7,7 +7,9 @@ import os
 import numpy as np
 import pytest
 
+import msccl_amd as M
 from oracle import loader as L
+from tests.gpu_harness import gen_inputs, to_torch
 
 pytestmark = pytest.mark.gpu
 
@@ -209,12 +211,13 @@ def _flat_env(monkeypatch, tree_max=None):
 @pytest.mark.parametrize("count", [1, 37, 511, 512, 4099])
 @pytest.mark.parametrize("dt", [7, 6, 9])
 def test_flat_tree_equals_the_chain_tree(monkeypatch, n, count, dt):
-    """Small AllReduces take the flat tree (all-pairs exchange, fold in the chain's order
-    x_{n-1} (+) ... (+) x_0) in the small kernel; the oracle is oracle/ring.py's chain tree."""
+    """Small AllReduces take the flat tree (every rank sends its input to every peer and folds the
+    n inputs in the chain's order x_{n-1} (+) ... (+) x_0, one hop) in the fold kernel
+    ("small" 2, interpreter.h: runFold); the oracle is oracle/ring.py's chain tree."""
     _flat_env(monkeypatch)
     rp = check(n, L.ALLREDUCE, count, dt, seed=5 + n)
     assert rp["algo"] == "tree"
-    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 1, rp["last"]
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
 
 
 @pytest.mark.parametrize("op,dt", [(1, 7), (2, 6), (3, 9), (0, 2), (1, 4), (2, 0)])
@@ -226,14 +229,78 @@ def test_flat_tree_ops(monkeypatch, op, dt, in_place):
 
 
 def test_flat_tree_multi_iteration_and_chain_knob(monkeypatch):
-    """Several interpreter iterations (8192 floats each; the general kernel when they do not
-    merge evenly); MSCCL_AMD_TREE_FLAT=0 keeps the chain; Avg (PreMulSum) always takes the chain."""
+    """Several FIFO steps per call (8192 floats a step, a ragged last one), repeated launches;
+    MSCCL_AMD_TREE_FLAT=0 keeps the chain; Avg (PreMulSum) always takes the chain."""
     _flat_env(monkeypatch, 256 << 10)
     rp = check(8, L.ALLREDUCE, 50001, 7, iters=2)
     assert rp["last"]["ringColl"] == 5, rp["last"]
     rp = check(8, L.ALLREDUCE, 8192 * 4, 7)
-    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 1, rp["last"]
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
     assert check(4, L.ALLREDUCE, 3001, 7, op=4)["last"]["ringColl"] == 4
     monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")
     rp = check(8, L.ALLREDUCE, 4099, 6)
     assert rp["algo"] == "tree" and rp["last"]["ringColl"] == 4, rp["last"]
+
+
+def test_flat_tree_across_ll_cleanup(monkeypatch):
+    """MSCCL_AMD_TEST_LL_CLEANUP=1 (8-bit flags, cleanup 8 steps in every 128): 300 fold-kernel
+    launches cross the flag wrap and the cleanup steps on every connection (the fold kernel stamps
+    its send slots' unused lines itself); Max is idempotent, so the in-place result stays the
+    chain tree's."""
+    _flat_env(monkeypatch)
+    monkeypatch.setenv("MSCCL_AMD_TEST_LL_CLEANUP", "1")
+    rp = check(4, L.ALLREDUCE, 4099, 6, op=2, iters=300)
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
+
+
+def _flat_proc(rank, world, count, q_in, q_out):
+    import torch
+    os.environ.pop("MSCCL_XML_FILES", None)
+    os.environ["NCCL_ALGO"] = "Ring,Tree"
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "30"
+    torch.cuda.set_device(0)
+    uid = M.get_unique_id() if rank == 0 else None
+    if rank == 0:
+        for _ in range(world - 1):
+            q_in.put(uid)
+    else:
+        uid = q_in.get(timeout=60)
+    x = gen_inputs(world, count, 7, 13)[rank]
+    comm = M.Comm.init_rank(world, uid, rank)
+    t = to_torch(x, torch.device("cuda:0"))
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(4):
+        comm.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, s)
+    torch.cuda.synchronize()
+    err = comm.async_error()
+    last = comm.info()["last"]
+    out = t.cpu().numpy()
+    comm.destroy()
+    q_out.put((rank, err, last["ringColl"], last["small"], out))
+
+
+def test_flat_tree_across_processes(monkeypatch):
+    """One rank per process (hipIpc FIFOs): each process launches its own fold kernel; the values
+    are the chain tree's (oracle/ring.py), 4 in-place AllReduces in a row."""
+    import torch.multiprocessing as mp
+    from oracle import ring as R
+    _flat_env(monkeypatch)   # inherited by the spawned ranks
+    world, count = 3, 1001
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_flat_proc, args=(r, world, count, q_in, q_out)) for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, ring_coll, small, out = q_out.get(timeout=300)
+        res[r] = (err, ring_coll, small, out)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    ins = gen_inputs(world, count, 7, 13)
+    for _ in range(4):
+        ins, _rp = R.run(L.ALLREDUCE, count, 7, 0, ins, [None] * world, True, 0)
+    for r in range(world):
+        assert res[r][0] == 0 and res[r][1] == 5 and res[r][2] == 2, res[r][:3]
+        assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))

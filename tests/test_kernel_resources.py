@@ -46,7 +46,14 @@ def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
     for k, v in hot.items():
         assert v.get("scratch", 1) == 0, (k, v)
     for k, v in ks.items():
-        assert v.get("vgpr", 999) <= 128, (k, v)
+        # the flat tree's fold kernel runs one or a few workgroups per rank, never co-resident
+        # with each other on a CU by necessity: __launch_bounds__(512, 1) allows 256 VGPRs
+        limit = 256 if "mscclFoldKernel" in k else 128
+        assert v.get("vgpr", 999) <= limit, (k, v)
+    fold = {k: v for k, v in ks.items() if re.search(r"mscclFoldKernelI(f|DF16_|NS_4Bf16E)Li[0-3]E", k)}
+    assert len(fold) == 3 * 4 * 2, sorted(fold)
+    for k, v in fold.items():
+        assert v.get("scratch", 1) == 0, (k, v)
     # the small-call kernel (fused exchange inside) for the same types and ops, both argument blocks
     small = {k: v for k, v in ks.items() if re.search(r"mscclSmallKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi0ELi(2|16)EE", k)}
     assert len(small) == 3 * 4 * 2, sorted(small)

@@ -14,7 +14,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("MSCCL_AMD_TRACE", "1")  # 2: start / end only, small kernel kept
+os.environ.setdefault("MSCCL_AMD_TRACE", "1")  # 2: small kernel kept (start, end + XCD)
 import msccl_amd as M  # noqa: E402
 from msccl_amd import xmlgen  # noqa: E402
 
@@ -62,6 +62,8 @@ def main():
                                                          int(e["arg"]) & 0xFFFFFF, t))
                 elif name in ("dep", "end"):
                     parts.append("%s#%d %.2f" % (name, e["step"], t))
+                elif name == "done" and os.environ.get("MSCCL_AMD_TRACE") == "2":
+                    parts.append("done %.2f xcc %d" % (t, int(e["arg"])))
                 else:
                     parts.append("%s %.2f" % (name, t))
             print("rank %d slot %3d: %s" % (r, s, " | ".join(parts)))

@@ -8,7 +8,7 @@
 # knob was not kept.)
 set -o pipefail
 export MSCCL_AMD_TIMEOUT_SEC=20
-OUT=gpurun_out/xcd
+OUT=${OUT:-gpurun_out/xcd}
 mkdir -p $OUT
 : > $OUT/summary.txt
 SZ=${SZ:-4194304,16777216,33554432}
@@ -28,11 +28,11 @@ import re, sys
 import numpy as np
 rows = []
 for l in open(sys.argv[1]):
-    m = re.search(r'slot\s+(\d+): start ([\d.]+) \| done ([\d.]+)', l)
+    m = re.search(r'slot\s+(\d+): start ([\d.]+) \| done ([\d.]+) xcc (\d+)', l)
     if m:
-        rows.append((int(m.group(1)), float(m.group(3))))
+        rows.append((int(m.group(4)), float(m.group(3))))
 a = np.array(rows)
-x = [a[a[:, 0] % 8 == k, 1].mean() for k in range(8)]
+x = [a[a[:, 0] == k, 1].mean() for k in range(8)]   # by the XCD the workgroup ran on (HW_REG_XCC_ID)
 print('pad %s: done median %.1f max %.1f; per-XCD mean %s' % (sys.argv[2], np.median(a[:, 1]), a[:, 1].max(), ' '.join('%.1f' % v for v in x)))
 PY
 done
