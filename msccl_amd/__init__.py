@@ -92,7 +92,8 @@ def lib() -> ctypes.CDLL:
     L.mscclAmdBootstrapAllgather.argtypes = [ctypes.POINTER(UniqueId), i, i, vp, sz, vp]
     L.mscclAmdAlgoBlocks.argtypes = [vp, i]
     L.mscclAmdTraceRead.argtypes = [vp, vp, sz, ctypes.POINTER(i), ctypes.POINTER(i)]
-    L.mscclAmdLineTearProbe.argtypes = [i, i, i, i, ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
+    if hasattr(L, "mscclAmdLineTearProbe"):  # MSCCL_AMD_LIB may name an older build (A/B runs)
+        L.mscclAmdLineTearProbe.argtypes = [i, i, i, i, ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
     _lib = L
     return L
 

@@ -36,6 +36,8 @@ constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-c
 constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kMaxSplit
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
 constexpr int kMaxFoldPeers = 15;      // flat tree fold: peers of one rank (MSCCL_MAX_REDUCE_FUSION 16 ranks)
+constexpr int kFlatSubs = 4;           // flat tree: sub-connections per peer = most fold workgroups per rank
+constexpr int kFoldPacksPerWg = 512;   // flat tree: a fold workgroup per 512 packs (8 KiB) of the call
 
 // Device trace event (mscclAmdTraceRead).
 struct TraceEvent {
@@ -180,8 +182,7 @@ struct RankWork {
   uint64_t* flags;
   uint64_t* epochs;
   int32_t maxSplit;
-  int16_t rotate;               // small kernel: workgroup b of the rank runs local slot (b + rotate) % nBlocks
-  int16_t pad0;                 // (MSCCL_AMD_XCD_ROTATE placement experiment; 0 = identity)
+  int32_t pad0;
   const char* images;           // thread-block images, tbStride bytes each
   int32_t tbStride;
   int32_t connSplit;            // connection record of (tb, sub): send / recv [tb * connSplit + sub]

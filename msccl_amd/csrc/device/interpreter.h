@@ -1272,7 +1272,8 @@ struct Interp {
 
   // ---------------------------------------------------------------- the flat tree (mscclFoldKernel)
   // The flat tree's one-hop AllReduce (transport.cc: ringUpload, plan.cc: makeFlatTreePlan), one
-  // workgroup per rank.  Per FIFO step every lane takes its 16-B packs of the input, stores each
+  // workgroup per 512 packs of the call (RankWork::split, at most kFlatSubs), each on contiguous
+  // packs and its own sub-connection of every peer.  Per FIFO step every lane takes its 16-B packs of the input, stores each
   // as two LL lines into every peer's slot (the send), then polls the same lines of every peer's
   // slot here and folds the n inputs in the order of thread block 0's reduction table: acc = x_0,
   // acc = fn(acc, x_i), the table listing ranks n-1 down to 0, i.e. the chain tree's x_{n-1} (+)
@@ -1282,7 +1283,7 @@ struct Interp {
   // (transport.cc: flatPeers); 8 peers' lines are polled per wait (VGPR addresses only: see
   // primitives.h ldLines16 on SGPR operands in asm).  No scratch, no flag, no second hop.  Its own kernel: the interpreter
   // kernels keep their register budget.
-  __device__ __forceinline__ void runFold(const RankWork& w, FoldShared* fs) {
+  __device__ __forceinline__ void runFold(const RankWork& w, int wg, FoldShared* fs) {
     tid = threadIdx.x;
     comm = w.comm;
     timeoutTicks = w.timeoutTicks;
@@ -1302,15 +1303,15 @@ struct Interp {
       for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
       if (tid >= 64 && tid < 64 + 4 * np) {
         const int k = (tid - 64) >> 2, j = (tid - 64) & 3;
-        ((u32x4*)&fs->foldSend[k])[j] = ((const u32x4*)(w.send + (size_t)(k + 1) * w.connSplit))[j];
+        ((u32x4*)&fs->foldSend[k])[j] = ((const u32x4*)(w.send + (size_t)(k + 1) * w.connSplit + wg))[j];
       }
       if (tid >= 192 && tid < 192 + 4 * np) {
         const int k = (tid - 192) >> 2, j = (tid - 192) & 3;
-        ((u32x4*)&fs->foldRecv[k])[j] = ((const u32x4*)(w.recv + (size_t)(k + 1) * w.connSplit))[j];
+        ((u32x4*)&fs->foldRecv[k])[j] = ((const u32x4*)(w.recv + (size_t)(k + 1) * w.connSplit + wg))[j];
       }
       if (tid == 128) {
         sh->aborted = 0;
-        sh->epoch = atomicLoadAgent(w.epochs);
+        sh->epoch = atomicLoadAgent(w.epochs + wg);  // slot (tb 0, sub wg)
       }
     }
     __syncthreads();
@@ -1332,7 +1333,11 @@ struct Interp {
     constexpr int E = 8 / TS;
     constexpr int G = 8;  // peers per wait
     const int n = (int)w.sizePerChunk;
-    const int npk = (n + PE - 1) / PE;
+    const int npkAll = (n + PE - 1) / PE;
+    // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges,
+    // cut into FIFO steps on its own sub-connection of every peer
+    const int p0 = (int)((int64_t)npkAll * wg / w.split);
+    const int npk = (int)((int64_t)npkAll * (wg + 1) / w.split) - p0;
     const int nlinesFull = (n + E - 1) / E;
     const __amdgpu_buffer_rsrc_t srs = makeRsrc(w.sendbuff), drs = makeRsrc(w.recvbuff);
     const bool vec = aligned16(w.sendbuff) && aligned16(w.recvbuff);
@@ -1360,7 +1365,7 @@ struct Interp {
       }
       __syncthreads();
       for (int q = tid; q < s1 - s0; q += kNT) {
-        const int B = s0 + q;
+        const int B = p0 + s0 + q;
         const bool two = 2 * B + 1 < nlinesFull;
         const u32x4 own = loadPack(srs, vec, B, n);
         const uint32_t o0 = (uint32_t)llLineIdx(q, 0) * 16;
@@ -1416,7 +1421,7 @@ struct Interp {
         const uint32_t f = fs->fold[k].sflag;
         for (int l = tid; l < slotLines; l += kNT) {
           const int q = ((l >> 7) << 6) + (l & 63), h = (l >> 6) & 1;
-          const bool used = s0 + q < s1 && 2 * (s0 + q) + h < nlinesFull;
+          const bool used = s0 + q < s1 && 2 * (p0 + s0 + q) + h < nlinesFull;
           if (!used) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, f, 0, f});
         }
       }
@@ -1431,12 +1436,12 @@ struct Interp {
     } while (s0 < npk);
     __syncthreads();
     if (tid < np) {  // persist the connections' steps (flat records of thread block k + 1)
-      DevSendConn* cg = w.send + (size_t)(tid + 1) * w.connSplit;
+      DevSendConn* cg = w.send + (size_t)(tid + 1) * w.connSplit + wg;
       cg->step = fs->foldSend[tid].step;
       cg->headSeen = fs->foldSend[tid].headSeen;
-      (w.recv + (size_t)(tid + 1) * w.connSplit)->step = fs->foldRecv[tid].step;
+      (w.recv + (size_t)(tid + 1) * w.connSplit + wg)->step = fs->foldRecv[tid].step;
     }
-    epilogue(w, 0, 0, workIndex);
+    epilogue(w, 0, wg, workIndex);
   }
   // index of the p-th peer in fold order (order: thread block per fold position, -1 = own input)
   static __device__ __forceinline__ int foldPeer(const int16_t* order, int nfold, int p) {
@@ -1584,19 +1589,21 @@ __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> 
   const RankWork& w = args.w[r];
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
-  int local = b - w.blockBase;
-  if (w.rotate != 0) local = (local + w.rotate) % w.nBlocks;
-  it.runSmall(w, local);
+  it.runSmall(w, b - w.blockBase);
 }
 
-// The flat tree's fold kernel (Interp::runFold): workgroup r runs rank r of the launch.
+// The flat tree's fold kernel (Interp::runFold): rank r of the launch owns workgroups
+// [blockBase, blockBase + nBlocks).
 template <typename T, int OP, int R>
 __global__ void __launch_bounds__(kNT, 1) mscclFoldKernel(const LaunchArgsN<R> args) {
   __shared__ BlockShared sh;
   __shared__ FoldShared fs;
+  const int b = blockIdx.x;
+  int r = 0;
+  while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
   Interp<T, OP, pLL> it;
   it.sh = &sh;
-  it.runFold(args.w[blockIdx.x], &fs);
+  it.runFold(args.w[r], b - args.w[r].blockBase, &fs);
 }
 
 }  // namespace msccl

@@ -45,7 +45,7 @@ int launchSmallKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
-// the flat tree's fold kernel (mscclFoldKernel, LL, Sum..Min): one workgroup per rank
+// the flat tree's fold kernel (mscclFoldKernel, LL, Sum..Min): RankWork::nBlocks workgroups per rank
 template <typename T, int OP>
 int launchFoldKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   constexpr int RC = kCompactLaunchRanks;
@@ -55,7 +55,7 @@ int launchFoldKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
       return 0;
     return n;
   }
-  if (gridBlocks != args.nRanks) return 1;  // one workgroup per rank (RankWork::nBlocks == 1)
+  if (gridBlocks < args.nRanks) return 1;  // every rank has at least one workgroup
   if (args.nRanks <= RC) {
     LaunchArgsN<RC> a;
     a.nRanks = args.nRanks;

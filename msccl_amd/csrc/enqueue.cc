@@ -197,7 +197,7 @@ RankWork makeFlatWork(Planned& p) {
   w.comm = comm->dComm;
   w.send = da.dSend;
   w.recv = da.dRecv;
-  w.connSplit = 1;
+  w.connSplit = da.connSplit;  // kFlatSubs sub-connections per peer
   w.images = da.dImages;
   w.tbStride = da.tbStride;
   w.timeoutTicks = comm->timeoutTicks;
@@ -212,9 +212,15 @@ RankWork makeFlatWork(Planned& p) {
   w.sizePerChunk = p.plan.sizePerChunk;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;
-  w.split = 1;
-  w.nBlocks = (int16_t)da.nBlocks;
+  // workgroups per rank: one per kFoldPacksPerWg packs of the call, at most kFlatSubs (a function
+  // of the call's size alone, so every rank picks the same and the two ends of every
+  // sub-connection own the same packs; MSCCL_AMD_FOLD_WGS lowers the cap, for measurements, and
+  // must then be set alike on every rank)
   const int64_t pe = 16 / refTypeSize(p.plan.dtype);
+  const int64_t npk = (p.plan.sizePerChunk + pe - 1) / pe;
+  static const int64_t maxWgs = std::max<int64_t>(1, std::min<int64_t>(kFlatSubs, envInt("MSCCL_AMD_FOLD_WGS", kFlatSubs)));
+  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(maxWgs, (npk + kFoldPacksPerWg - 1) / kFoldPacksPerWg));
+  w.split = (uint8_t)wgs;
   w.maxOpElems = (int64_t)kMaxRunSlots * (comm->llSlotLines / 2) * pe;
   int merge = 1;
   if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {  // makeWork's rule, send runs of one chunk
@@ -222,12 +228,12 @@ RankWork makeFlatWork(Planned& p) {
     merge = (int)std::max<int64_t>(1, std::min<int64_t>(64, w.maxOpElems / chunk));
   }
   w.merge = (uint8_t)merge;
-  w.nBlocks = 1;  // mscclFoldKernel: one workgroup per rank (interpreter.h: runFold)
+  w.nBlocks = (int16_t)wgs;  // mscclFoldKernel (interpreter.h: runFold)
   w.foldPeers = (uint8_t)(comm->nRanks - 1);
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.launchSeq = comm->workIndex++;
-  comm->last = {-1, p.plan.proto, 1, merge, kTreeFlat, 0, w.nBlocks};
+  comm->last = {-1, p.plan.proto, wgs, merge, kTreeFlat, 0, w.nBlocks};
   return w;
 }
 
@@ -352,14 +358,6 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   }
   args.nRanks = (int)ps.size();
   if (blocks == 0) return ncclSuccess;
-  {
-    // MSCCL_AMD_XCD_ROTATE=K: co-resident rank i's workgroups run slots shifted by i * K (a
-    // placement experiment: workgroups are dealt to XCDs by grid index; the small kernel only)
-    static const int64_t rot = envInt("MSCCL_AMD_XCD_ROTATE", 0);
-    if (rot != 0)
-      for (size_t i = 0; i < ps.size(); i++)
-        if (args.w[i].nBlocks > 0) args.w[i].rotate = (int16_t)((rot * (int64_t)i) % args.w[i].nBlocks);
-  }
   EventPool& pool = tEvents[dev];
   pool.used = 0;
   for (size_t i = 1; i < ps.size(); i++) {

@@ -41,7 +41,8 @@ uint8_t groupProtoMask(const ncclComm* comm, int group) {
 }
 
 int groupSubs(const ncclComm* comm, int group) {
-  if (group == kRingGroup || group == kTreeGroup || group == kFlatGroup) return 1;  // the fallbacks run unsplit
+  if (group == kFlatGroup) return kFlatSubs;  // one per fold workgroup (interpreter.h: runFold)
+  if (group == kRingGroup || group == kTreeGroup) return 1;  // the ring / tree fallbacks run unsplit
   return comm->algoSplit.empty() ? 1 : comm->algoSplit[group];
 }
 // The tree fallback's chain (rank order, root 0): thread block 2c+0 reduces up (receives from
@@ -474,7 +475,7 @@ ncclResult_t ringUpload(ncclComm* comm) {
     DevAlgoHost& d = comm->ringAlgos[5];
     d.nBlocks = 1;
     d.tbStride = (int)imageBytes(1, 0, order.size());
-    d.connSplit = 1;
+    d.connSplit = kFlatSubs;
     d.dSend = comm->flatSend;
     d.dRecv = comm->flatRecv;
     std::vector<char> img((size_t)d.tbStride, 0);
