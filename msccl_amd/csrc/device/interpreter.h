@@ -152,6 +152,14 @@ struct Interp {
     }
   }
 
+  // MSCCL_LAT_TRACE (a measurement build, tools/lat_trace.py): timestamps at fixed points of a
+  // small call.  Each point is a global store, whose completion later vmcnt(0) waits include, so
+  // the points shift the times they measure by up to a store's round trip.
+#ifdef MSCCL_LAT_TRACE
+#define LAT_EV(T) ev((T), 0, 0)
+#else
+#define LAT_EV(T) ((void)0)
+#endif
   __device__ __forceinline__ void ev(uint16_t type, uint16_t step, uint32_t arg) {
     if (trace != nullptr && tid == 0 && nev < maxEv) {
       TraceEvent e;
@@ -408,11 +416,13 @@ struct Interp {
     int B[U];
     bool act[U], two[U];
     u32x4 v[U];  // source of the step being received
+    LAT_EV(11);
     waitSendCredit<kLLFifoSlots>();
     llStepPacks(s, slotPacks, nlinesFull, 0, B, act, two);
 #pragma unroll
     for (int u = 0; u < U; u++) v[u] = act[u] ? loadPack(srs, vec, B[u], s.n) : (u32x4){0, 0, 0, 0};
     llSendLines(s, slotLines, nlinesFull, 0, min(s.npk, slotPacks), act, two, v);
+    LAT_EV(12);
     for (int k = 0; k < nsteps; k++) {
       const int j = k + 1;
       const bool snd = j < nsteps;
@@ -448,9 +458,11 @@ struct Interp {
         const u32x4 peer = {ln[2 * u].x, ln[2 * u].z, ln[2 * u + 1].x, ln[2 * u + 1].z};
         if (act[u]) storePack(drs, vec, B[u], s.n, F::pack(peer, v[u]));  // rrc: fn(peer, local)
       }
+      LAT_EV(13);
       recvStep++;
       __syncthreads();
       if (tid == 0) atomicStoreSys(rc->remoteHead, recvStep);
+      LAT_EV(14);
       if (snd) {
         llSendLines(s, slotLines, nlinesFull, j * slotPacks, min(s.npk, (j + 1) * slotPacks), as, ts, vs);
 #pragma unroll
@@ -1476,6 +1488,12 @@ struct Interp {
     DevTbHeader hd;
     const uint64_t workIndex = prologue(w, bid, sub, hd);
     const int maxSplit = w.maxSplit;
+#ifdef MSCCL_LAT_TRACE
+    trace = w.trace ? w.trace + (size_t)(bid * maxSplit + sub) * w.traceEvents : nullptr;
+    nev = 1;
+    maxEv = w.traceEvents;
+    LAT_EV(10);
+#endif
     T* const bufs[3] = {(T*)w.sendbuff, (T*)w.recvbuff, (T*)w.scratch};
     // element offsets stay below 2^30 (smallEligible: at most 1 GiB per buffer), so 32 bits
     const int sizePer = (int)w.sizePerChunk;
@@ -1543,7 +1561,20 @@ struct Interp {
       for (int grid = 0, iter = 0; grid < sizePer; grid += nelem, iter++)
         if (!runPass(grid, iter)) break;
     }
+    LAT_EV(15);
     epilogue(w, bid, sub, workIndex);
+#ifdef MSCCL_LAT_TRACE
+    LAT_EV(16);
+    if (trace != nullptr && tid == 0) {
+      TraceEvent e;
+      e.ts = tStart;
+      e.type = kEvHeader;
+      e.step = (uint16_t)nev;
+      e.arg = (uint32_t)workIndex;
+      trace[0] = e;
+    }
+    return;
+#endif
     if (w.trace != nullptr && tid == 0) {
       // light trace (MSCCL_AMD_TRACE=2): this workgroup's start, and its end with the XCD it ran on
       // (HW_REG_XCC_ID: the dispatch order only says which blocks share an XCD, not which one)
