@@ -7,7 +7,9 @@
 set -o pipefail
 TAG=${1:-r01}
 shift
-ARGS=${@:-"--no-cpu --quiet --sizes 33554432 --steps 20 --warmup 5"}
+# --pmc off: under rocprofv3 the bench must not start its own profiler child (an exec from a process
+# the outer profiler has initialised); --no-secondary: every interpreter dispatch is a headline launch
+ARGS=${@:-"--no-cpu --quiet --sizes 33554432 --steps 20 --warmup 5 --pmc off --no-secondary"}
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
