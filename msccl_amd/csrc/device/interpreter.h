@@ -1282,6 +1282,16 @@ struct Interp {
     }
   }
 
+  // pack B of block `blk` (n elements each) of a buffer of consecutive blocks
+  __device__ __forceinline__ u32x4 loadBlockPack(const T* base, int blk, int n, int B) {
+    const T* b = base + (size_t)blk * n;
+    return loadPack(makeRsrc(b), aligned16(b), B, n);
+  }
+  __device__ __forceinline__ void storeBlockPack(T* base, int blk, int n, int B, u32x4 x) {
+    T* b = base + (size_t)blk * n;
+    storePack(makeRsrc(b), aligned16(b), B, n, x);
+  }
+
   // ---------------------------------------------------------------- the flat tree (mscclFoldKernel)
   // The flat tree's one-hop AllReduce (transport.cc: ringUpload, plan.cc: makeFlatTreePlan), one
   // workgroup per 512 packs of the call (RankWork::split, at most kFlatSubs), each on contiguous
@@ -1334,8 +1344,15 @@ struct Interp {
       raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
       __builtin_memcpy(&hd, &raw, sizeof(hd));
     }
-    const DevTransfer t = loadTransfer((const DevTransfer*)&sh->img[1]);
-    const int16_t* order = (const int16_t*)((const DevTransfer*)&sh->img[1] + hd.nsteps) + 2 * hd.ndeps + t.redPtr;
+    // the collective (RankWork::ringColl): 0 the AllReduce (the flat tree), kRingReduceScatter,
+    // kRingAllGather; the image's transfers 0 / 1 carry the AllReduce / ReduceScatter fold orders
+    // and transfer 2 the rank of every peer record (then this rank) (transport.cc: ringUpload)
+    const int mode = w.ringColl;
+    const DevTransfer* tr0 = (const DevTransfer*)&sh->img[1];
+    const int16_t* reds = (const int16_t*)(tr0 + hd.nsteps) + 2 * hd.ndeps;
+    const DevTransfer t = loadTransfer(tr0 + (mode == kRingReduceScatter ? 1 : 0));
+    const int16_t* order = reds + t.redPtr;
+    const int16_t* rankOf = reds + loadTransfer(tr0 + 2).redPtr;
     const int nfold = t.numReds;
     int ownAt = 0, nq = 0;  // peers folded before the own input
     for (int i = 0; i < nfold; i++) {
@@ -1379,14 +1396,63 @@ struct Interp {
       for (int q = tid; q < s1 - s0; q += kNT) {
         const int B = p0 + s0 + q;
         const bool two = 2 * B + 1 < nlinesFull;
-        const u32x4 own = loadPack(srs, vec, B, n);
         const uint32_t o0 = (uint32_t)llLineIdx(q, 0) * 16;
         const uint32_t o1 = two ? (uint32_t)llLineIdx(q, 1) * 16 : o0;
-        for (int k = 0; k < np; k++) {  // the send: this pack to every peer
-          const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[k].out);
-          const uint32_t f = fs->fold[k].sflag;
-          st16<kAuxFifo>(frs, o0, (u32x4){own.x, f, own.y, f});
-          if (two) st16<kAuxFifo>(frs, o1, (u32x4){own.z, f, own.w, f});
+        u32x4 own;
+        if (mode == kRingReduceScatter) {
+          // the send: block rank(k) of the input to peer k, 8 peers' packs loaded per batch
+          for (int g0 = 0; g0 < np; g0 += G) {
+            u32x4 v[G];
+#pragma unroll
+            for (int k = 0; k < G; k++)
+              if (g0 + k < np) v[k] = loadBlockPack((const T*)w.sendbuff, uni((int)rankOf[g0 + k]), n, B);
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              if (g0 + k >= np) continue;
+              const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[g0 + k].out);
+              const uint32_t f = fs->fold[g0 + k].sflag;
+              st16<kAuxFifo>(frs, o0, (u32x4){v[k].x, f, v[k].y, f});
+              if (two) st16<kAuxFifo>(frs, o1, (u32x4){v[k].z, f, v[k].w, f});
+            }
+          }
+          own = loadBlockPack((const T*)w.sendbuff, uni((int)rankOf[np]), n, B);
+        } else {
+          own = loadPack(srs, vec, B, n);
+          for (int k = 0; k < np; k++) {  // the send: this pack to every peer
+            const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[k].out);
+            const uint32_t f = fs->fold[k].sflag;
+            st16<kAuxFifo>(frs, o0, (u32x4){own.x, f, own.y, f});
+            if (two) st16<kAuxFifo>(frs, o1, (u32x4){own.z, f, own.w, f});
+          }
+        }
+        if (mode == kRingAllGather) {
+          // every peer's pack to its block of the output, peers in record order, 8 per wait
+          for (int g0 = 0; g0 < np; g0 += G) {
+            const void* la[2 * G];
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              const char* in = (const char*)fs->fold[g0 + k < np ? g0 + k : g0].in;
+              la[2 * k] = in + o0;
+              la[2 * k + 1] = in + o1;
+            }
+            u32x4 ln[2 * G];
+            ldLines16(la, ln);
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              if (g0 + k >= np) continue;
+              const uint32_t rflag = fs->fold[g0 + k].rflag;
+              Spin spins;
+              while (ln[2 * k].y != rflag || ln[2 * k].w != rflag || ln[2 * k + 1].y != rflag ||
+                     ln[2 * k + 1].w != rflag) {
+                if (spinAbort(spins)) break;
+                ldLines2(la[2 * k], la[2 * k + 1], ln[2 * k], ln[2 * k + 1]);
+              }
+              storeBlockPack((T*)w.recvbuff, uni((int)rankOf[g0 + k]), n, B,
+                             (u32x4){ln[2 * k].x, ln[2 * k].z, ln[2 * k + 1].x, ln[2 * k + 1].z});
+            }
+          }
+          storeBlockPack((T*)w.recvbuff, uni((int)rankOf[np]), n, B, own);
+          continue;
         }
         u32x4 acc = (u32x4){0, 0, 0, 0};
         bool first = true;

@@ -95,7 +95,7 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
       if (flatEnabled(comm)) makeFlatTreePlan(c, comm->knobs, &out->plan);
       INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; %s fallback (%s, %d channels)",
            op.coll, op.count, (int)op.dtype,
-           out->plan.ringColl == kTreeFlat ? "flat tree" : out->plan.ringColl == kTreeAllReduce ? "tree" : "ring",
+           out->plan.ringColl == kTreeFlat ? "flat" : out->plan.ringColl == kTreeAllReduce ? "tree" : "ring",
            out->plan.proto == kProtoLL ? "LL" : "Simple", out->plan.ringChannels);
       return ncclSuccess;
     }
@@ -229,6 +229,8 @@ RankWork makeFlatWork(Planned& p) {
   }
   w.merge = (uint8_t)merge;
   w.nBlocks = (int16_t)wgs;  // mscclFoldKernel (interpreter.h: runFold)
+  // the kernel's collective: 0 the flat tree's AllReduce, else kRingReduceScatter / kRingAllGather
+  w.ringColl = (uint8_t)(p.plan.flatColl == kRingAllReduce ? 0 : p.plan.flatColl);
   w.foldPeers = (uint8_t)(comm->nRanks - 1);
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;

@@ -244,9 +244,22 @@ static int makeTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
 }
 
 int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
-  if (!k.treeFlat || p->ringColl != kTreeAllReduce || p->proto != kProtoLL || c.redop > kDevMin ||
-      c.nRanks < 2 || c.nRanks > kMaxReduceFusion || p->nBytes > (1ll << 30))
+  if (!k.treeFlat || p->proto != kProtoLL || c.nRanks < 2 || c.nRanks > kMaxReduceFusion || p->nBytes > (1ll << 30))
     return 1;
+  int mode;
+  if (p->ringColl == kTreeAllReduce) {
+    if (c.redop > kDevMin) return 1;
+    mode = kRingAllReduce;
+  } else if (p->ringColl == kRingReduceScatter || p->ringColl == kRingAllGather) {
+    if (p->ringColl == kRingReduceScatter && c.redop > kDevMin) return 1;  // pre / post ops: the ring
+    // one hop instead of the ring's n - 1 while latency dominates (a rank's block up to the tree's
+    // per-rank default, 16 KiB, or MSCCL_AMD_TREE_MAX_BYTES)
+    const int64_t lim = k.treeMaxBytes >= 0 ? k.treeMaxBytes : 16384;
+    if (p->nBytes / c.nRanks > lim) return 1;
+    mode = p->ringColl;
+  } else {
+    return 1;
+  }
   // It runs in its own kernel (interpreter.h: runFold) as one call over the whole buffer (at
   // most 1 GiB: 32-bit offsets); the fields below keep the MSCCL plan's form for introspection,
   // sizePerChunk = count being what the kernel reads.  Chunk math of makePlan for LL (enqueue.cc:591-734,
@@ -255,6 +268,7 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   const int nt = p->refNthreads;
   const int64_t stepSize = k.buffSizes[kProtoLL] / kFifoSteps;
   p->ringColl = kTreeFlat;
+  p->flatColl = mode;
   p->ringChannels = 0;
   p->nchunksPerLoop = 1;
   p->sizeMultiplier = 1;

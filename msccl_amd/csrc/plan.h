@@ -46,6 +46,9 @@ struct Plan {
   int ringColl = 0;
   int ringChannels = 0;
   int64_t ringLastChunk = 0;  // LL ReduceScatter / AllGather lastChunkSize (elements)
+  // ringColl == kTreeFlat: the collective the fold kernel runs (kRingAllReduce for the flat tree,
+  // kRingReduceScatter / kRingAllGather for the flat forms of the ring's)
+  int flatColl = 0;
 };
 
 // Every environment knob the per-call planning reads, captured once at communicator init
@@ -92,11 +95,15 @@ int chooseSplit(int maxBlocks, int coResident, const Knobs& k);
 // 0, or returns ncclInvalidUsage when the collective / op has no ring (AllToAll, custom, Avg).
 // Channels, protocol and thread count are this build's choice (oracle/ring.py: ring_params).
 int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p);
-// The flat tree (kTreeFlat): a tree AllReduce plan (makeRingPlan chose the tree, LL, op Sum..Min,
-// 2..16 ranks) turned into a one-iteration-per-chunk MSCCL plan of the flat program
-// (transport.cc: ringUpload): every rank sends its input to every peer, and one workgroup folds
-// the n inputs straight from the FIFOs in the chain tree's order x_{n-1} (+) x_{n-2} (+) ... (+)
-// x_0 (interpreter.h: foldRecv), one hop instead of 2 (n - 1).  Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).
+// The flat forms (kTreeFlat, run by mscclFoldKernel, interpreter.h: runFold), one hop each:
+//   a tree AllReduce plan (makeRingPlan chose the tree, LL, op Sum..Min, 2..16 ranks): every rank
+//   sends its input to every peer and folds the n inputs in the chain tree's order x_{n-1} (+)
+//   x_{n-2} (+) ... (+) x_0, instead of 2 (n - 1) hops;
+//   an LL ring ReduceScatter (op Sum..Min) or AllGather of at most MSCCL_AMD_TREE_MAX_BYTES per
+//   rank's block (default 16 KiB): every rank sends block p to peer p and folds its own block in
+//   the ring's order x_{r+1} (+) x_{r+2} (+) ... (+) x_{r+n-1} (+) x_r (ReduceScatter), or sends
+//   its block to every peer and stores each peer's at its place (AllGather), instead of n - 1.
+// Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).
 int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p);
 
 }  // namespace msccl

@@ -444,47 +444,59 @@ ncclResult_t ringUpload(ncclComm* comm) {
     NCCLCHECK(uploadImages(img, &d));
   }
   if (flatEnabled(comm)) {
-    // The flat tree (plan.cc: makeFlatTreePlan), run by mscclFoldKernel (interpreter.h: runFold),
-    // one workgroup per rank: it sends its input to every peer p_j over the flat connections of
-    // thread block 1 + j (flatPeers) and folds every rank's input, in the order x_{n-1}, ...,
-    // x_0: acc = x_{n-1}, acc = fn(acc, x_q) for q = n - 2 down to 0.  The order is the one
-    // image uploaded here: thread block 0's reduction table, one entry per rank from n - 1 down
-    // to 0, the thread block whose connections carry that rank (-1: this rank's own input).
-    // That is the chain tree's fold (runTreeSplit on the chain, transport.cc: treePeers): leaf
-    // n - 1 sends its input up, rank q folds fn(child's partial, x_q), the root's result comes
-    // back down.  Every op admitted (Sum, Prod, Max, Min) is commutative per element, so the
-    // values are the tree's bit for bit, whatever side of fn each operand sits on.  One hop: no
-    // scratch, no dependency flag, no copy.
+    // The flat forms (plan.cc: makeFlatTreePlan), run by mscclFoldKernel (interpreter.h:
+    // runFold): each rank exchanges with every peer p_j over the flat connections of thread block
+    // 1 + j (flatPeers) in one hop.  The AllReduce folds every rank's input in the order x_{n-1},
+    // ..., x_0: acc = x_{n-1}, acc = fn(acc, x_q) for q = n - 2 down to 0, the chain tree's fold
+    // (runTreeSplit on the chain, transport.cc: treePeers: leaf n - 1 sends its input up, rank q
+    // folds fn(child's partial, x_q), the root's result comes back down).  Every op admitted (Sum,
+    // Prod, Max, Min) is commutative per element, so the values are the tree's bit for bit,
+    // whatever side of fn each operand sits on; the same holds for the ReduceScatter's ring order.
+    // No scratch, no dependency flag, no copy.
     const int r = comm->rank;
     std::vector<int> sp, rp;
     flatPeers(r, n, &sp, &rp);
-    Transfer fold;
-    fold.type = kFoldRecv;
-    fold.srcbuf = kInput;
-    fold.dstbuf = kOutput;
-    fold.count = 1;
-    std::vector<int16_t> order;
-    for (int q = n - 1; q >= 0; q--) {
-      int tb = -1;
+    // Three tables in the image's reduction list, one transfer each:
+    //   0: the AllReduce fold order (thread block per position, ranks n-1 .. 0, -1 = own input);
+    //   1: the ReduceScatter fold order, the ring's for this rank's block (reduce_scatter.h:13-67:
+    //      the block starts at rank r+1 and is reduced at r+2, ..., r+n-1, then here): ranks r+1,
+    //      ..., r+n-1, then the own input;
+    //   2: the rank each peer record k (thread block k + 1) connects, then this rank.
+    auto tbOf = [&](int q) {
       for (int b = 1; b < n; b++)
-        if (rp[b] == q) tb = b;
-      order.push_back((int16_t)(q == r ? -1 : tb));
+        if (rp[b] == q) return b;
+      return -1;
+    };
+    std::vector<int16_t> reds;
+    for (int q = n - 1; q >= 0; q--) reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
+    for (int i = 1; i <= n; i++) {
+      const int q = (r + i) % n;
+      reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
     }
-    fold.numReds = (int16_t)order.size();
-    fold.redPtr = 0;
+    for (int b = 1; b < n; b++) reds.push_back((int16_t)rp[b]);
+    reds.push_back((int16_t)r);
+    std::vector<Transfer> ts(3);
+    for (int i = 0; i < 3; i++) {
+      ts[i].type = kFoldRecv;
+      ts[i].srcbuf = kInput;
+      ts[i].dstbuf = kOutput;
+      ts[i].count = 1;
+      ts[i].numReds = (int16_t)n;
+      ts[i].redPtr = (int16_t)(i * n);
+    }
     DevAlgoHost& d = comm->ringAlgos[5];
     d.nBlocks = 1;
-    d.tbStride = (int)imageBytes(1, 0, order.size());
+    d.tbStride = (int)imageBytes(ts.size(), 0, reds.size());
     d.connSplit = kFlatSubs;
     d.dSend = comm->flatSend;
     d.dRecv = comm->flatRecv;
     std::vector<char> img((size_t)d.tbStride, 0);
     DevTbHeader h;
     memset(&h, 0, sizeof(h));
-    h.nsteps = 1;
-    h.nreds = (uint16_t)order.size();
+    h.nsteps = (uint16_t)ts.size();
+    h.nreds = (uint16_t)reds.size();
     const std::vector<int16_t> none;
-    putImage(img, 0, h, std::vector<Transfer>{fold}, none, none, order);
+    putImage(img, 0, h, ts, none, none, reds);
     NCCLCHECK(uploadImages(img, &d));
   }
   return ncclSuccess;

@@ -253,6 +253,53 @@ def test_flat_tree_across_ll_cleanup(monkeypatch):
     assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
 
 
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("count", [1, 37, 512, 4099])
+@pytest.mark.parametrize("in_place", [True, False])
+def test_flat_reduce_scatter_equals_the_ring(monkeypatch, n, count, in_place):
+    """LL ReduceScatters of at most 16 KiB per rank's block take the fold kernel's one hop: block
+    p to peer p, the own block folded in the ring's order x_{r+1} (+) ... (+) x_{r+n-1} (+) x_r;
+    the oracle is oracle/ring.py's ring (reduce_scatter.h:13-67), bit for bit."""
+    _flat_env(monkeypatch)
+    rp = check(n, L.REDUCE_SCATTER, count, 7, in_place=in_place, seed=7 + n)
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8, 16])
+@pytest.mark.parametrize("count", [1, 37, 512, 8191])
+@pytest.mark.parametrize("in_place", [True, False])
+def test_flat_all_gather_equals_the_ring(monkeypatch, n, count, in_place):
+    """LL AllGathers of at most 16 KiB per rank take the fold kernel: every rank's block to every
+    peer, each stored at its place (all_gather.h:13-78's result)."""
+    _flat_env(monkeypatch)
+    rp = check(n, L.ALLGATHER, count, 6, in_place=in_place, seed=9 + n)
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
+
+
+@pytest.mark.parametrize("op,dt", [(1, 6), (2, 9), (3, 2), (0, 8), (2, 0)])
+def test_flat_reduce_scatter_ops_and_limits(monkeypatch, op, dt):
+    """Ops Sum..Min on other types, repeated launches; a block over the limit takes the ring, and
+    Avg (PreMulSum) always does."""
+    _flat_env(monkeypatch)
+    rp = check(4, L.REDUCE_SCATTER, 1001, dt, op=op, in_place=False, iters=3)
+    assert rp["last"]["ringColl"] == 5, rp["last"]
+    _flat_env(monkeypatch, 1024)
+    rp = check(4, L.REDUCE_SCATTER, 1001, dt, op=op)
+    assert rp["last"]["ringColl"] == 2, rp["last"]
+    _flat_env(monkeypatch)
+    assert check(4, L.REDUCE_SCATTER, 1001, 7, op=4)["last"]["ringColl"] == 2
+    monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")
+    assert check(4, L.ALLGATHER, 1001, 7)["last"]["ringColl"] == 3
+
+
+def test_flat_all_gather_across_ll_cleanup(monkeypatch):
+    """300 in-place AllGathers across the 8-bit flag wrap and cleanup steps."""
+    _flat_env(monkeypatch)
+    monkeypatch.setenv("MSCCL_AMD_TEST_LL_CLEANUP", "1")
+    rp = check(3, L.ALLGATHER, 2047, 0, iters=300)
+    assert rp["last"]["ringColl"] == 5 and rp["last"]["small"] == 2, rp["last"]
+
+
 def _flat_proc(rank, world, count, q_in, q_out):
     import torch
     os.environ.pop("MSCCL_XML_FILES", None)

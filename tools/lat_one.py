@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--proto", default="LL")
     ap.add_argument("--dtype", type=int, default=7)
     ap.add_argument("--iters", type=int, default=300)
+    ap.add_argument("--coll", default="ar", choices=["ar", "rs", "ag"],
+                    help="AllReduce, or ReduceScatter / AllGather with --bytes per rank's block "
+                         "(fallback schedules only; fbring there is the ring, fbtree the flat form)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the launches in one hipGraph and time its replay: device time per launch "
                          "without the host's per-call cost")
@@ -32,6 +35,10 @@ def main():
         os.environ["NCCL_ALGO"] = "Ring" if a.schedule == "fbring" else "Tree"
         if a.schedule == "fbchain":   # the chain tree (fbtree: the flat tree where it applies)
             os.environ["MSCCL_AMD_TREE_FLAT"] = "0"
+        if a.coll != "ar":           # the ring, or (fbtree) its flat form
+            os.environ["NCCL_ALGO"] = "Ring,Tree"
+            if a.schedule == "fbring":
+                os.environ["MSCCL_AMD_TREE_FLAT"] = "0"
     else:
         path = "/tmp/lat_one_%d.xml" % os.getpid()
         open(path, "w").write(gen[a.schedule]())
@@ -40,13 +47,19 @@ def main():
     ts = {7: 4, 6: 2, 9: 2}[a.dtype]
     cnt = a.bytes // ts
     bufs = [torch.ones(cnt * ts // 4 + 1, device="cuda") for _ in comms]
+    big = [torch.ones(cnt * a.ranks * ts // 4 + 1, device="cuda") for _ in comms] if a.coll != "ar" else None
 
     stream = torch.cuda.Stream()
 
     def step():
         with M.group():
-            for c, b in zip(comms, bufs):
-                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, stream.cuda_stream)
+            for i, (c, b) in enumerate(zip(comms, bufs)):
+                if a.coll == "ar":
+                    c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, stream.cuda_stream)
+                elif a.coll == "rs":
+                    c.reduce_scatter(big[i].data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, stream.cuda_stream)
+                else:
+                    c.all_gather(b.data_ptr(), big[i].data_ptr(), cnt, a.dtype, stream.cuda_stream)
     for _ in range(20):
         step()
     torch.cuda.synchronize()
@@ -71,8 +84,8 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize()
     last = comms[0].info()["last"]
-    print("%s %d B x%d ranks: %.2f us per launch (events%s), host %.2f us per call; ran ringColl %d small %d" % (
-        a.schedule, a.bytes, a.ranks, e0.elapsed_time(e1) * 1000 / a.iters, ", graph replay" if graph else "",
+    print("%s%s %d B x%d ranks: %.2f us per launch (events%s), host %.2f us per call; ran ringColl %d small %d" % (
+        a.schedule, "" if a.coll == "ar" else "-" + a.coll, a.bytes, a.ranks, e0.elapsed_time(e1) * 1000 / a.iters, ", graph replay" if graph else "",
         host * 1e6, last["ringColl"], last["small"]), flush=True)
     for c in comms:
         c.destroy()
