@@ -53,6 +53,7 @@ struct alignas(16) FoldShared {
     const LLLine* in;   // recv slot of this step
     uint32_t sflag, rflag;
   } fold[kMaxFoldPeers];
+  uint8_t perm[kMaxFoldPeers + 1];  // peer record of each fold position (the own input skipped)
 };
 
 __device__ __forceinline__ uint64_t computeFlag(uint64_t workIndex, uint64_t iter, uint64_t step) {
@@ -1356,8 +1357,12 @@ struct Interp {
     const int nfold = t.numReds;
     int ownAt = 0, nq = 0;  // peers folded before the own input
     for (int i = 0; i < nfold; i++) {
-      if (uni((int)order[i]) < 0) ownAt = nq;
-      else nq++;
+      const int b = uni((int)order[i]);
+      if (b < 0) ownAt = nq;
+      else {
+        if (tid == 0) fs->perm[nq] = (uint8_t)(b - 1);  // read after the first step's barrier
+        nq++;
+      }
     }
     constexpr int E = 8 / TS;
     constexpr int G = 8;  // peers per wait
@@ -1461,7 +1466,7 @@ struct Interp {
           int pk[G];
 #pragma unroll
           for (int k = 0; k < G; k++) {
-            pk[k] = foldPeer(order, nfold, g0 + k < nq ? g0 + k : g0);
+            pk[k] = fs->perm[g0 + k < nq ? g0 + k : g0];
             const char* in = (const char*)fs->fold[pk[k]].in;
             la[2 * k] = in + o0;
             la[2 * k + 1] = in + o1;
@@ -1520,17 +1525,6 @@ struct Interp {
       (w.recv + (size_t)(tid + 1) * w.connSplit + wg)->step = fs->foldRecv[tid].step;
     }
     epilogue(w, 0, wg, workIndex);
-  }
-  // index of the p-th peer in fold order (order: thread block per fold position, -1 = own input)
-  static __device__ __forceinline__ int foldPeer(const int16_t* order, int nfold, int p) {
-    int j = 0, k = 0;
-    for (int i = 0; i < nfold; i++) {
-      const int b = order[i];
-      if (b < 0) continue;
-      if (j == p) k = b - 1;
-      j++;
-    }
-    return k;
   }
 
   // ---------------------------------------------------------------- small calls
