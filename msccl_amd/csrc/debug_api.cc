@@ -53,6 +53,12 @@ int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, si
   return putOut(o.str(), out, outLen);
 }
 
+// the collective the fold kernel would run for this fallback plan (plan.cc: makeFlatTreePlan;
+// kRingAllReduce / kRingReduceScatter / kRingAllGather), 0 when the call keeps the ring / chain
+static int flatOf(const CallDesc& c, const Knobs& k, Plan rp) {
+  return makeFlatTreePlan(c, k, &rp) == 0 ? rp.flatColl : 0;
+}
+
 int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_t count, int dtype, int redop,
                      int inPlace, char* out, size_t outLen) {
   std::vector<Algorithm> algos;
@@ -76,7 +82,7 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
       o << ",\"ring\":{\"coll\":" << rp.ringColl << ",\"proto\":" << rp.proto << ",\"channels\":" << rp.ringChannels
         << ",\"nthreads\":" << rp.refNthreads << ",\"size\":" << rp.count << ",\"dtype\":" << rp.dtype
         << ",\"nBytes\":" << rp.nBytes << ",\"chunk\":" << rp.chunkSize << ",\"minChunk\":" << rp.minChunk
-        << ",\"lastChunk\":" << rp.ringLastChunk << "}";
+        << ",\"lastChunk\":" << rp.ringLastChunk << ",\"flat\":" << flatOf(c, k, rp) << "}";
     o << "}";
     return putOut(o.str(), out, outLen);
   }

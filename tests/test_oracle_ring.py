@@ -175,3 +175,30 @@ def test_tree_oracle_exact_and_chain_order(monkeypatch, dt, n):
     for r in range(n - 2, -1, -1):
         acc = N.apply(0, 7, acc, ins[r])
     assert np.array_equal(res[0].view(np.uint32), acc.view(np.uint32))
+
+
+def test_flat_routing(tmp_path, monkeypatch):
+    """Which fallback calls the one-hop fold kernel takes (plan.cc makeFlatTreePlan; "flat" is the
+    collective it runs: 1 AllReduce, 2 ReduceScatter, 3 AllGather, 0 = the ring / chain tree)."""
+    p = tmp_path / "none.xml"
+    p.write_text(xmlgen.allreduce_allpairs(2, 1, "LL", max_bytes=1))
+    monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES")
+
+    def flat(n, coll, count, dt, op=0):
+        return M.plan_json(str(p), 0, n, coll, count, dt, op, True)["ring"]["flat"]
+    # ReduceScatter / AllGather: a rank's block up to 16 KiB; pre / post ops keep the ring
+    assert flat(8, L.REDUCE_SCATTER, 4096, 7) == 2
+    assert flat(8, L.REDUCE_SCATTER, 4097, 7) == 0
+    assert flat(8, L.REDUCE_SCATTER, 1000, 7, op=4) == 0
+    assert flat(4, L.REDUCE_SCATTER, 1000, 2, op=3) == 2
+    assert flat(16, L.ALLGATHER, 8192, 6) == 3
+    assert flat(16, L.ALLGATHER, 8193, 6) == 0
+    assert flat(17, L.ALLGATHER, 100, 6) == 0      # at most 16 ranks
+    # AllReduce: the tree's calls (16 KiB per rank), Sum..Min
+    assert flat(8, L.ALLREDUCE, 4096 * 8, 7) == 1
+    assert flat(8, L.ALLREDUCE, 4096 * 8 + 1, 7) == 0
+    assert flat(8, L.ALLREDUCE, 1000, 7, op=4) == 0
+    monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", "1024")
+    assert flat(2, L.REDUCE_SCATTER, 256, 7) == 2 and flat(2, L.REDUCE_SCATTER, 257, 7) == 0
+    monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")
+    assert flat(2, L.REDUCE_SCATTER, 256, 7) == 0 and flat(2, L.ALLREDUCE, 256, 7) == 0
