@@ -252,10 +252,9 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
     mode = kRingAllReduce;
   } else if (p->ringColl == kRingReduceScatter || p->ringColl == kRingAllGather) {
     if (p->ringColl == kRingReduceScatter && c.redop > kDevMin) return 1;  // pre / post ops: the ring
-    // one hop instead of the ring's n - 1 while latency dominates (a rank's block up to the tree's
-    // per-rank default, 16 KiB, or MSCCL_AMD_TREE_MAX_BYTES)
-    const int64_t lim = k.treeMaxBytes >= 0 ? k.treeMaxBytes : 16384;
-    if (p->nBytes / c.nRanks > lim) return 1;
+    // one hop instead of the ring's n - 1 over the whole LL range (profiles/r03_fold_xover.txt:
+    // 8 ranks 64 KiB per rank 41.6 -> 17.6 us), or a rank's block up to MSCCL_AMD_TREE_MAX_BYTES
+    if (k.treeMaxBytes >= 0 && p->nBytes / c.nRanks > k.treeMaxBytes) return 1;
     mode = p->ringColl;
   } else {
     return 1;
@@ -290,11 +289,11 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   // ring thread block runs 2(n-1), so the tree wins while latency dominates.  Measured on
   // co-resident ranks, fp16 (profiles/r02_fallback_ring_tree.txt): 2 ranks 128 B 11.7 -> 8.0 us,
   // 64 KiB ring ahead (16.3 vs 18.1); 8 ranks 128 B 35.9 -> 17.7 us, 64 KiB 52.6 -> 45.3 us,
-  // 1 MiB ring ahead (64 vs 85).  Default threshold: 16 KiB per rank.
-  const int64_t treeMax = k.treeMaxBytes >= 0 ? k.treeMaxBytes : (int64_t)16384 * c.nRanks;
-  const bool tree = c.coll == kAllReduce && k.treeOn &&
-                    (!k.ringOn || (int64_t)c.count * refTypeSize(c.dtype) <= treeMax);
-  if (!tree && !k.ringOn) return 5;
+  // 1 MiB ring ahead (64 vs 85).  Default threshold: 16 KiB per rank.  Calls the tree then runs
+  // as the flat tree (makeFlatTreePlan: LL, Sum..Min, 2..16 ranks) take it over the whole LL
+  // range (512 KiB): the one-hop fold kernel beats the LL ring there (fp16, co-resident,
+  // profiles/r03_fold_xover.txt: 2 ranks 256 KiB 60.0 -> 25.3 us, 8 ranks 64 KiB 60.8 -> 16.4,
+  // 16 ranks 256 KiB 129 -> 108).
   if (c.coll == kAllReduce) p->ringColl = kRingAllReduce;
   else if (c.coll == kReduceScatter) p->ringColl = kRingReduceScatter;
   else if (c.coll == kAllGather) p->ringColl = kRingAllGather;
@@ -304,6 +303,14 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   const bool llOk = k.protoOn[kProtoLL], simpleOk = k.protoOn[kProtoSimple];
   if (!llOk && !simpleOk) return 5;
   p->proto = (llOk && (p->nBytes <= (512 << 10) || !simpleOk)) ? kProtoLL : kProtoSimple;
+  const bool flatTree = k.treeFlat && p->proto == kProtoLL && c.redop <= kDevMin && c.nRanks >= 2 &&
+                        c.nRanks <= kMaxReduceFusion;
+  const int64_t treeMax = k.treeMaxBytes >= 0 ? k.treeMaxBytes
+                          : flatTree          ? (int64_t)(512 << 10)
+                                              : (int64_t)16384 * c.nRanks;
+  const bool tree = c.coll == kAllReduce && k.treeOn &&
+                    (!k.ringOn || (int64_t)c.count * refTypeSize(c.dtype) <= treeMax);
+  if (!tree && !k.ringOn) return 5;
   const int64_t forced = k.ringChannels;
   int64_t ch = forced > 0 ? forced : std::max<int64_t>(1, p->nBytes >> 18);
   p->ringChannels = (int)std::max<int64_t>(1, std::min<int64_t>(kRingChannels, ch));

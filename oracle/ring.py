@@ -22,7 +22,8 @@ msccl_amd/csrc/plan.cc (makeRingPlan) mirrors it:
   * channels = min(32, max(1, nBytes >> 18)) (MSCCL_AMD_RING_CHANNELS forces it);
   * LL when nBytes <= 512 KiB, else Simple (NCCL_PROTO masks them; LL128 is not used here);
   * nThreads is not reduced for small messages (the reference halves it below its thresholds);
-  * AllReduce calls of at most MSCCL_AMD_TREE_MAX_BYTES (default 16 KiB per rank), or all of them when
+  * AllReduce calls of at most MSCCL_AMD_TREE_MAX_BYTES (default 16 KiB per rank; 512 KiB, the LL
+    range, where the flat tree runs them: LL, ops Sum..Min, 2..16 ranks), or all of them when
     NCCL_ALGO enables Tree but not Ring, take the tree: the reference's runTreeSplit
     (all_reduce.h:174-276) on a chain in rank order (root 0, parent r-1, child r+1), with
     computeColl's tree chunk math (enqueue.cc:634-644; tree depth = nranks) and the kernel's
@@ -91,7 +92,7 @@ def tree_params(rp: dict, nranks: int) -> dict:
     return out
 
 
-def ring_params(coll: int, count: int, dtype: int, nranks: int) -> Optional[dict]:
+def ring_params(coll: int, count: int, dtype: int, nranks: int, op: int = 0) -> Optional[dict]:
     """Host-side decisions for one fallback call: interpreter dtype/size (elements of one rank's
     block), nBytes, proto, channels, nthreads, chunkSize and, for LL ReduceScatter/AllGather,
     lastChunkSize (elements)."""
@@ -132,7 +133,9 @@ def ring_params(coll: int, count: int, dtype: int, nranks: int) -> Optional[dict
           "algo": "ring"}
     tree_max = int(os.environ.get("MSCCL_AMD_TREE_MAX_BYTES", "-1") or -1)
     if tree_max < 0:
-        tree_max = 16384 * nranks
+        flat = int(os.environ.get("MSCCL_AMD_TREE_FLAT", "1") or 1) != 0 and proto == L.PROTO_LL and \
+            op <= 3 and 2 <= nranks <= 16
+        tree_max = RING_LL_MAX_BYTES if flat else 16384 * nranks
     ring_ok, tree_ok = _algo_enabled("Ring"), _algo_enabled("Tree")
     if coll == L.ALLREDUCE and tree_ok and (not ring_ok or count * N.type_size(dtype) <= tree_max):
         return tree_params(rp, nranks)
@@ -235,7 +238,7 @@ def run(coll: int, count: int, dtype: int, op: int, inputs: Sequence[np.ndarray]
     outputs[r]=None except for AllGather, whose output buffer holds the input at rank*count.
     Returns (outputs, params)."""
     n = len(inputs)
-    rp = ring_params(coll, count, dtype, n)
+    rp = ring_params(coll, count, dtype, n, op)
     size, dt = rp["size"], rp["dtype"]
     ins, outs = [], []
     for r in range(n):

@@ -192,10 +192,15 @@ def test_tree_threshold_and_repeats(monkeypatch):
     the same communicators; repeated launches keep both connection sets in step."""
     monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", str(64 << 10))
     assert check(4, L.ALLREDUCE, 5000, 7, iters=5)["algo"] == "tree"
-    monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES")        # default: 16 KiB per rank
+    monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES")        # default: the LL range for the flat tree
+    assert check(4, L.ALLREDUCE, 131072, 7)["last"]["ringColl"] == 5
+    assert check(4, L.ALLREDUCE, 131073, 7)["algo"] == "ring"
+    assert check(4, L.ALLREDUCE, 50000, 7, iters=2)["last"]["ringColl"] == 5
+    assert check(4, L.ALLREDUCE, 16384, 7, op=4)["algo"] == "tree"   # Avg: 16 KiB per rank
+    assert check(4, L.ALLREDUCE, 16385, 7, op=4)["algo"] == "ring"
+    monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")         # without the flat tree: 16 KiB per rank
     assert check(4, L.ALLREDUCE, 16384, 7)["algo"] == "tree"
     assert check(4, L.ALLREDUCE, 16385, 7)["algo"] == "ring"
-    assert check(4, L.ALLREDUCE, 50000, 7, iters=2)["algo"] == "ring"
 
 
 # ---- flat tree: the chain tree's values in one hop (plan.cc: makeFlatTreePlan) -------------------

@@ -186,18 +186,25 @@ def test_flat_routing(tmp_path, monkeypatch):
 
     def flat(n, coll, count, dt, op=0):
         return M.plan_json(str(p), 0, n, coll, count, dt, op, True)["ring"]["flat"]
-    # ReduceScatter / AllGather: a rank's block up to 16 KiB; pre / post ops keep the ring
-    assert flat(8, L.REDUCE_SCATTER, 4096, 7) == 2
-    assert flat(8, L.REDUCE_SCATTER, 4097, 7) == 0
+    # ReduceScatter / AllGather: the LL range (512 KiB in all); pre / post ops keep the ring
+    assert flat(8, L.REDUCE_SCATTER, 16384, 7) == 2
+    assert flat(8, L.REDUCE_SCATTER, 16385, 7) == 0
     assert flat(8, L.REDUCE_SCATTER, 1000, 7, op=4) == 0
     assert flat(4, L.REDUCE_SCATTER, 1000, 2, op=3) == 2
-    assert flat(16, L.ALLGATHER, 8192, 6) == 3
-    assert flat(16, L.ALLGATHER, 8193, 6) == 0
+    assert flat(16, L.ALLGATHER, 16384, 6) == 3
+    assert flat(16, L.ALLGATHER, 16385, 6) == 0
     assert flat(17, L.ALLGATHER, 100, 6) == 0      # at most 16 ranks
-    # AllReduce: the tree's calls (16 KiB per rank), Sum..Min
-    assert flat(8, L.ALLREDUCE, 4096 * 8, 7) == 1
-    assert flat(8, L.ALLREDUCE, 4096 * 8 + 1, 7) == 0
+    # AllReduce, Sum..Min: the tree takes the LL range where the flat tree runs it
+    assert flat(8, L.ALLREDUCE, 131072, 7) == 1
+    r = M.plan_json(str(p), 0, 8, L.ALLREDUCE, 131073, 7, 0, True)["ring"]
+    assert r["flat"] == 0 and r["coll"] == 1
     assert flat(8, L.ALLREDUCE, 1000, 7, op=4) == 0
+    # Avg (PreMulSum): the chain tree up to 16 KiB per rank, then the ring
+    assert M.plan_json(str(p), 0, 8, L.ALLREDUCE, 32768, 7, 4, True)["ring"]["coll"] == 4
+    assert M.plan_json(str(p), 0, 8, L.ALLREDUCE, 32769, 7, 4, True)["ring"]["coll"] == 1
+    for cnt, op in ((131072, 0), (131073, 0), (32768, 4), (32769, 4)):
+        want = "tree" if cnt in (131072, 32768) else "ring"
+        assert R.ring_params(L.ALLREDUCE, cnt, 7, 8, op)["algo"] == want
     monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", "1024")
     assert flat(2, L.REDUCE_SCATTER, 256, 7) == 2 and flat(2, L.REDUCE_SCATTER, 257, 7) == 0
     monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")
