@@ -105,13 +105,19 @@ def spawn_ranks(n: int, argv) -> int:
     return subprocess.call(cmd)
 
 
-def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only: bool = False, fused=()):
+def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only: bool = False, fused=(),
+                   l2_reuse: bool = True):
     """Algorithmic HBM bytes and wire bytes of one launch for one rank (whole schedule).
     payload_only counts FIFO traffic at its payload size (LL flags / LL128 flag words excluded).
     fused: thread blocks whose s + rrc exchange ran fused (comm info "algoFuse"): the rrc reuses
-    the source the s read, one read of B less."""
+    the source the s read, one read of B less.
+    l2_reuse: the same source chunks sent by several thread blocks of the launch (one block to k
+    peers: an all-pairs AllGather, the two-phase AllReduce's reduced chunk) are read from HBM once;
+    the other k - 1 reads are served by L2 (PMC: the 8-rank AllGather read 0.775x and the C3 shape
+    0.947x of the byte model that counted every read, profiles/r03_extras8_pmc.json)."""
     f = 1.0 if payload_only else {0: 2.0, 1: 4.0 / 3.0}.get(proto, 1.0)  # LL: 8 B data per 16-B line
     hbm = wire = 0
+    sent = set()
     for b_i, tb in enumerate(algo["tbs"]):
         first_s = b_i in fused and proto == 0
         for t in tb["transfers"]:
@@ -119,9 +125,13 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only:
             b = cnt * size_per * ts
             if typ == 0:      # s
                 hbm += b + f * b; wire += f * b
+                key = (t[1], t[2], cnt)
                 if first_s:
                     hbm -= b
                     first_s = False
+                elif l2_reuse and key in sent:
+                    hbm -= b
+                sent.add(key)
             elif typ == 1:    # r
                 hbm += f * b + b
             elif typ == 2:    # rcs
@@ -222,15 +232,29 @@ def cpu_baseline(n: int, nbytes: int, dt: int, seconds: float):
             "ms_per_allreduce": round(t * 1e3, 4)}
 
 
+def config_id(n: int, proto: str, dtname: str) -> str:
+    """The BASELINE.json config an all-pairs AllReduce sweep of n ranks is: C2 (2 ranks, LL, fp32),
+    C3 (8 ranks, LL, fp16), or none ("" : a shape of its own)."""
+    if proto == "LL" and n == 2 and dtname == "fp32":
+        return "C2"
+    if proto == "LL" and n == 8 and dtname == "fp16":
+        return "C3"
+    return ""
+
+
 def workload_desc(multi: bool, n: int, proto: str, dtname: str, one_gpu: bool = False) -> str:
+    cid = config_id(n, proto, dtname)
     if not multi:
-        return ("C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
+        return ("%s%d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
+                "(fused launch, local HBM in place of xGMI)" % (cid + " shape: " if cid else "", n, proto, dtname)
+                if cid != "C2" else
+                "C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
                 "(fused launch, local HBM in place of xGMI)" % (n, proto, dtname))
     if one_gpu:
         return ("rehearsal: %d rank processes sharing one MI355X (hipIpc FIFOs, local HBM in place of "
                 "xGMI), all-pairs %s AllReduce, %s" % (n, proto, dtname))
     return ("%s: %d-rank all-pairs %s AllReduce over xGMI, %s, one rank per GPU"
-            % ("C3" if n == 8 else "C2-family", n, proto, dtname))
+            % (cid or "%d-GPU" % n, n, proto, dtname))
 
 
 TIER_KINDS = {"a": "allreduce_allpairs (two-phase: s, r, re, s, r; msccl-tools form)",
@@ -772,7 +796,9 @@ def main():
             "kernel": "%s<%s,Sum,%s>" % ("mscclSmallKernel" if headline_small else "mscclKernel", dtname, a.proto),
             "algorithmic_bytes_per_launch": head["hbm_bytes_per_rank"] * ranks_on_gpu,
             "kernel_ms": head["kernel_ms"]}
-    if multi:
+    if multi and not one_gpu and world > 1:
+        # the xGMI roofline only where the ranks are on different GPUs (a one-GPU rehearsal's
+        # "links" are local HBM: a fraction of the xGMI peak would not be a measurement)
         link = XGMI_LINK_GBS * (n - 1)
         roof["xgmi"] = {"busbw": head["busbw"], "peak": link, "frac": round(head["busbw"] / link, 4),
                         "ll_ceiling": round(link * {0: 0.5, 1: 0.75}.get(proto_id, 1.0), 1),

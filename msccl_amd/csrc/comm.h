@@ -48,6 +48,10 @@ struct DevAlgoHost {
   DevSendConn* dSend = nullptr;
   DevRecvConn* dRecv = nullptr;
   int connSplit = 1;
+  // this schedule's range of dependency-flag / launch-epoch slots (init.cc: allocSlots): a launch
+  // reads and advances only its own schedule's epochs
+  int slotBase = 0;
+  int slotCount = 0;
 };
 
 // A thread block whose exchange with its single peer may run fused (transport.cc: fusableTbs):
@@ -96,7 +100,8 @@ struct ncclComm {
   int buffSizes[3] = {0, 0, 0};
 
   // MSCCL state
-  uint64_t* dFlags = nullptr;
+  uint64_t* dFlags = nullptr;            // [slotTotal][kFlagStride] flags, then [slotTotal] epochs
+  int slotTotal = 0;
   msccl::TraceEvent* dTrace = nullptr;   // MSCCL_AMD_TRACE: [216 * maxSplit][traceEvents]
   int traceEvents = 0;
   bool traceLight = false;               // MSCCL_AMD_TRACE=2: start / end per workgroup, small kernel kept

@@ -33,7 +33,6 @@ constexpr int kMaxRunSlots = 4;
 constexpr int kMaxLaunchRanks = 16;    // ranks fused into one launch (same device, same group)
 constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag padding)
 constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
-constexpr int kFlagSlots = 216 * kMaxSplit;  // MSCCL_MAX_NUM_THREAD_BLOCKS x kMaxSplit
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
 constexpr int kMaxFoldPeers = 15;      // flat tree fold: peers of one rank (MSCCL_MAX_REDUCE_FUSION 16 ranks)
 constexpr int kFlatSubs = 4;           // flat tree: sub-connections per peer = most fold workgroups per rank
@@ -131,20 +130,21 @@ struct DevRecvConn {
 static_assert(sizeof(DevSendConn) == 64 && sizeof(DevRecvConn) == 64, "connection records are four 16-B units");
 
 struct DevComm {
-  uint64_t* flags;              // [kFlagSlots * kFlagStride]
+  uint64_t* flags;              // [slots][kFlagStride]: every schedule's range (ncclComm::slotTotal)
   volatile uint32_t* abortFlag; // host-mapped
   uint32_t* errWord;            // host-mapped: 0 ok, else error code (1 timeout, 2 bad program)
   uint64_t timeoutTicks;        // s_memrealtime ticks (100 MHz) a single wait may last; 0 = for ever
   int32_t maxSplit;             // sub-connections per (channel, peer): conn k of key c = send[c*maxSplit+k]
   int32_t pad;
   // Launch epoch (the reference's host-side workIndex, enqueue.cc:714-721, kept on the device so
-  // that a captured hipGraph replays correctly), one word per workgroup slot
-  // (slot = tb * maxSplit + sub, the flag index): a workgroup reads its own slot at start and
-  // writes slot + 1 at its end, together with the slots this launch does not run (tbs beyond
-  // the schedule's, subs beyond its split).  Every slot therefore holds the same value at every
-  // launch start, and no counter is shared by the workgroups of a launch (a contended
-  // "last one out" counter cost several us per launch at 512 workgroups).
-  uint64_t* epochs;             // [kFlagSlots]
+  // that a captured hipGraph replays correctly), one word per workgroup slot of every schedule
+  // (slot = tb * maxSplit + sub within the schedule's range, the flag index): a workgroup reads
+  // its own slot at start and writes slot + 1 at its end, together with the slots of its schedule
+  // this launch does not run (subs beyond its split, ring channels beyond its count).  Every slot
+  // of a schedule therefore holds the same value at each of its launch starts, no counter is
+  // shared by the workgroups of a launch (a contended "last one out" counter cost several us per
+  // launch at 512 workgroups), and a launch writes no other schedule's words.
+  uint64_t* epochs;             // [slots]
   uint64_t* unused;
   // NPKit-style trace (null = off): [slot = tb * maxSplit + sub][traceEvents]
   struct TraceEvent* trace;
@@ -197,6 +197,7 @@ struct RankWork {
   uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
   uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
   uint8_t foldPeers;            // flat tree (mscclFoldKernel): peers, on the records of thread blocks 1..foldPeers
+  int16_t epochSlots;           // the schedule's flag / epoch slots (flags and epochs point at its range)
   int64_t maxOpElems;           // largest run of sends before a receive (elements, all sub-connections)
   // ring fallback (kRingNone for MSCCL schedules): the program's offsets are chunk / rank indices
   // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)

@@ -990,9 +990,10 @@ struct Interp {
   }
 
   // Epilogue: persist the connection state and advance this slot's epoch, plus the epoch of
-  // every slot this launch does not run (DevComm::epochs): the subs [split, maxSplit) of each
-  // launched tb (by that tb's sub 0), and the slots of the tbs beyond the schedule's,
-  // [nTb * maxSplit, kFlagSlots), dealt over the launch's workgroups.
+  // every slot of the schedule's range this launch does not run (DevComm::epochs): the subs
+  // [split, maxSplit) of each launched tb (by that tb's sub 0), and the slots of the tbs beyond
+  // this launch's, [nTb * maxSplit, epochSlots) (ring / tree channels not used by this call),
+  // dealt over the launch's workgroups.  An MSCCL schedule always runs all its tbs: nothing there.
   __device__ __forceinline__ void epilogue(const RankWork& w, int bid, int sub, uint64_t workIndex) {
     const int split = w.split, maxSplit = w.maxSplit;
     __syncthreads();
@@ -1009,7 +1010,7 @@ struct Interp {
     }
     const int launched = w.nBlocks, nTb = launched / split, g = bid * split + sub;
     if (sub == 0 && tid < maxSplit - split) atomicStoreAgent(w.epochs + bid * maxSplit + split + tid, workIndex + 1);
-    for (int j = nTb * maxSplit + g + tid * launched; j < kFlagSlots; j += kNT * launched)
+    for (int j = nTb * maxSplit + g + tid * launched; j < w.epochSlots; j += kNT * launched)
       atomicStoreAgent(w.epochs + j, workIndex + 1);
   }
 
@@ -1035,6 +1036,20 @@ struct Interp {
   template <bool FUSE>
   __device__ __forceinline__ bool exec(const DevTransfer& t, T* srcP, T* dstP, int64_t srcoff, int64_t dstoff,
                                        int64_t reOff, int64_t sizePer, const Shape& s) {
+#ifdef MSCCL_EXP_COMPACT
+    // measurement build: the small kernel with the pair exchange's transfers only (code size A/B)
+    if constexpr (FUSE) {
+      switch (t.type) {
+        case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
+        case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
+        case tSendRrc:
+          if constexpr (PROTO == pLL && OP <= 3) [[clang::always_inline]] llFusedOp(srcP + srcoff, dstP + dstoff, s);
+          break;
+        default: return false;
+      }
+      return true;
+    }
+#endif
     switch (t.type) {
       case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
       case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, s); break;
@@ -1308,13 +1323,27 @@ struct Interp {
   // kernels keep their register budget.
   __device__ __forceinline__ void runFold(const RankWork& w, int wg, FoldShared* fs) {
     tid = threadIdx.x;
+    t0 = __builtin_amdgcn_s_memrealtime();
     comm = w.comm;
     timeoutTicks = w.timeoutTicks;
     llFlagMask = w.llFlagMask;
     llCleanMask = w.llCleanMask;
     redArg = 0;
-    trace = nullptr;
+    // MSCCL_AMD_TRACE: the workgroup's setup, its one pass as one primitive, its end (slot wg);
+    // NPKit: the launch's time sync and the pass as one RECV_REDUCE_COPY_SEND (tb 0's buffer)
+    trace = w.trace ? w.trace + (size_t)wg * w.traceEvents : nullptr;
+    nev = 1;
+    maxEv = w.traceEvents;
     nkBuf = nullptr;
+    if (w.npkit != nullptr && wg == 0) {
+      const NpkitLog* lg = w.npkit;
+      nkCap = lg->cap;
+      nkBuf = lg->events;
+      nkHeadG = lg->heads;
+      nkHead = uni(*nkHeadG);
+      nk(NPKIT_EVENT_TIME_SYNC_CPU, 0, (uint64_t)(npkitTicksToNs(t0, lg->clockKHz) + lg->cpuOffsetNs));
+      nk(NPKIT_EVENT_TIME_SYNC_GPU, 0, t0);
+    }
     scG = nullptr;
     rcG = nullptr;
     const int np = w.foldPeers;
@@ -1334,7 +1363,7 @@ struct Interp {
       }
       if (tid == 128) {
         sh->aborted = 0;
-        sh->epoch = atomicLoadAgent(w.epochs + wg);  // slot (tb 0, sub wg)
+        sh->epoch = atomicLoadAgent(w.epochs + wg);  // slot wg of the fold's range
       }
     }
     __syncthreads();
@@ -1377,6 +1406,9 @@ struct Interp {
     const bool vec = aligned16(w.sendbuff) && aligned16(w.recvbuff);
     const int slotLines = uni(fs->foldRecv[0].llSlotLines);
     const int slotPacks = slotLines / 2;
+    ev(kEvSetup, 0, 0);
+    ev(kEvPrimBegin, 0, ((uint32_t)tRRCS << 24) | (uint32_t)min(npk * PE, 0xFFFFFF));
+    nk(NPKIT_EVENT_RECV_REDUCE_COPY_SEND_ENTRY, (uint64_t)n * TS);
     int s0 = 0;
     do {
       const int s1 = npk - s0 < slotPacks ? npk : s0 + slotPacks;
@@ -1517,6 +1549,8 @@ struct Interp {
       }
       s0 = s1;
     } while (s0 < npk);
+    nk(NPKIT_EVENT_RECV_REDUCE_COPY_SEND_EXIT, (uint64_t)n * TS);
+    ev(kEvPrimEnd, 0, 0);
     __syncthreads();
     if (tid < np) {  // persist the connections' steps (flat records of thread block k + 1)
       DevSendConn* cg = w.send + (size_t)(tid + 1) * w.connSplit + wg;
@@ -1524,7 +1558,22 @@ struct Interp {
       cg->headSeen = fs->foldSend[tid].headSeen;
       (w.recv + (size_t)(tid + 1) * w.connSplit + wg)->step = fs->foldRecv[tid].step;
     }
-    epilogue(w, 0, wg, workIndex);
+    // the epochs: the fold's workgroups own slots [0, split) of its range (kFlatSubs slots); slots
+    // [split, epochSlots) are advanced for the workgroups this call does not run
+    __syncthreads();
+    const int wgs = w.split;
+    if (tid == 0) atomicStoreAgent(w.epochs + wg, workIndex + 1);
+    for (int j = wgs + wg + tid * wgs; j < w.epochSlots; j += kNT * wgs) atomicStoreAgent(w.epochs + j, workIndex + 1);
+    if (nkBuf != nullptr && tid == 0) *nkHeadG = nkHead;
+    ev(kEvEnd, 0, 0);
+    if (trace != nullptr && tid == 0) {
+      TraceEvent h;
+      h.ts = t0;
+      h.type = kEvHeader;
+      h.step = (uint16_t)nev;
+      h.arg = (uint32_t)workIndex;
+      trace[0] = h;
+    }
   }
 
   // ---------------------------------------------------------------- small calls
@@ -1615,7 +1664,11 @@ struct Interp {
       }
       return true;
     };
+#ifdef MSCCL_EXP_COMPACT
+    if (false) {
+#else
     if (whole) {
+#endif
       runPass(0, 0);  // the common small call: no pass loop state
     } else {
       for (int grid = 0, iter = 0; grid < sizePer; grid += nelem, iter++)

@@ -165,8 +165,9 @@ RankWork makeRingWork(Planned& p) {
   w.npkit = comm->dNpkit;
   w.redOpArg = p.op.redArg;
   w.redOpArgIsPtr = p.op.redArgIsPtr;
-  w.flags = comm->dFlags;
-  w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  w.flags = comm->dFlags + (size_t)da.slotBase * kFlagStride;
+  w.epochs = comm->dFlags + (size_t)comm->slotTotal * kFlagStride + da.slotBase;
+  w.epochSlots = (int16_t)da.slotCount;
   w.maxSplit = comm->maxSplit;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;
@@ -206,20 +207,19 @@ RankWork makeFlatWork(Planned& p) {
   w.trace = comm->dTrace;
   w.traceEvents = comm->traceEvents;
   w.npkit = comm->dNpkit;
-  w.flags = comm->dFlags;
-  w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  w.flags = comm->dFlags + (size_t)da.slotBase * kFlagStride;
+  w.epochs = comm->dFlags + (size_t)comm->slotTotal * kFlagStride + da.slotBase;
+  w.epochSlots = (int16_t)da.slotCount;
   w.maxSplit = comm->maxSplit;
   w.sizePerChunk = p.plan.sizePerChunk;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;
   // workgroups per rank: one per kFoldPacksPerWg packs of the call, at most kFlatSubs (a function
   // of the call's size alone, so every rank picks the same and the two ends of every
-  // sub-connection own the same packs; MSCCL_AMD_FOLD_WGS lowers the cap, for measurements, and
-  // must then be set alike on every rank)
+  // sub-connection own the same packs; one workgroup against up to four: profiles/r03_ab_fold_wgs_and_r02.txt)
   const int64_t pe = 16 / refTypeSize(p.plan.dtype);
   const int64_t npk = (p.plan.sizePerChunk + pe - 1) / pe;
-  static const int64_t maxWgs = std::max<int64_t>(1, std::min<int64_t>(kFlatSubs, envInt("MSCCL_AMD_FOLD_WGS", kFlatSubs)));
-  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(maxWgs, (npk + kFoldPacksPerWg - 1) / kFoldPacksPerWg));
+  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(kFlatSubs, (npk + kFoldPacksPerWg - 1) / kFoldPacksPerWg));
   w.split = (uint8_t)wgs;
   w.maxOpElems = (int64_t)kMaxRunSlots * (comm->llSlotLines / 2) * pe;
   int merge = 1;
@@ -263,8 +263,9 @@ RankWork makeWork(Planned& p) {
   w.npkit = comm->dNpkit;
   w.redOpArg = p.op.redArg;
   w.redOpArgIsPtr = p.op.redArgIsPtr;
-  w.flags = comm->dFlags;
-  w.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  w.flags = comm->dFlags + (size_t)da.slotBase * kFlagStride;
+  w.epochs = comm->dFlags + (size_t)comm->slotTotal * kFlagStride + da.slotBase;
+  w.epochSlots = (int16_t)da.slotCount;
   w.maxSplit = comm->maxSplit;
   w.sizePerChunk = p.plan.sizePerChunk;
   w.chunkSize = p.plan.chunkSize;

@@ -59,14 +59,6 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
   *comm->hostErr = 0;
   NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devAbort, comm->hostAbort, 0), "hipHostGetDevicePointer"));
   NCCLCHECK(hipErr(hipHostGetDevicePointer((void**)&comm->devErr, comm->hostErr, 0), "hipHostGetDevicePointer"));
-  // flags, then one launch-epoch word per workgroup slot
-  const size_t flagWords = (size_t)kFlagSlots * kFlagStride + kFlagSlots;
-  NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, flagWords * sizeof(uint64_t)), "hipMalloc flags"));
-  NCCLCHECK(hipErr(hipMemset(comm->dFlags, 0, flagWords * sizeof(uint64_t)), "hipMemset"));
-  // flags start at 0, the first launch runs epoch 1 (the reference's workIndex, init.cc:300-302)
-  const std::vector<uint64_t> epoch0(kFlagSlots, 1);
-  NCCLCHECK(hipErr(hipMemcpy(comm->dFlags + (size_t)kFlagSlots * kFlagStride, epoch0.data(),
-                             kFlagSlots * sizeof(uint64_t), hipMemcpyHostToDevice), "hipMemcpy epoch"));
   comm->workIndex = 1;  // flags start at 0 (init.cc:300-302)
   NCCLCHECK(hipErr(hipEventCreateWithFlags(&comm->doneEvent, hipEventDisableTiming), "hipEventCreate"));
   // scratch = max over algorithms of maxBytes * s_chunks / nchunksperloop (init.cc:809-835)
@@ -211,8 +203,35 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   return ncclSuccess;
 }
 
+// Dependency flags and launch epochs (the reference's mscclFlag array and workIndex,
+// init.cc:300-304): every schedule (each loaded algorithm, each ring / tree program, the flat
+// fold) owns a range of slots, one per workgroup it can run (thread blocks x maxSplit; the fold:
+// kFlatSubs).  A launch reads its epoch from its own slot and advances its own range only
+// (interpreter.h: epilogue), so no launch touches another schedule's words.
+static ncclResult_t allocSlots(ncclComm* comm) {
+  int total = 0;
+  auto take = [&](DevAlgoHost& d, int count) {
+    d.slotBase = total;
+    d.slotCount = count;
+    total += count;
+  };
+  for (DevAlgoHost& d : comm->devAlgos) take(d, std::max(1, d.nBlocks) * comm->maxSplit);
+  for (int k = 0; k < 5; k++) take(comm->ringAlgos[k], std::max(1, comm->ringAlgos[k].nBlocks) * comm->maxSplit);
+  take(comm->ringAlgos[5], kFlatSubs);
+  comm->slotTotal = total;
+  const size_t flagWords = (size_t)total * kFlagStride + total;
+  NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, flagWords * sizeof(uint64_t)), "hipMalloc flags"));
+  NCCLCHECK(hipErr(hipMemset(comm->dFlags, 0, flagWords * sizeof(uint64_t)), "hipMemset"));
+  // flags start at 0, the first launch runs epoch 1 (the reference's workIndex, init.cc:300-302)
+  const std::vector<uint64_t> epoch0(total, 1);
+  NCCLCHECK(hipErr(hipMemcpy(comm->dFlags + (size_t)total * kFlagStride, epoch0.data(), total * sizeof(uint64_t),
+                             hipMemcpyHostToDevice), "hipMemcpy epoch"));
+  return ncclSuccess;
+}
+
 ncclResult_t commFinish(ncclComm* comm) {
   NCCLCHECK(algoUpload(comm));
+  NCCLCHECK(allocSlots(comm));
   DevComm dc;
   memset(&dc, 0, sizeof(dc));
   dc.flags = comm->dFlags;
@@ -232,7 +251,7 @@ ncclResult_t commFinish(ncclComm* comm) {
     dc.traceEvents = comm->traceEvents;
   }
   NCCLCHECK(npkitSetup(comm));
-  dc.epochs = comm->dFlags + (size_t)kFlagSlots * kFlagStride;
+  dc.epochs = comm->dFlags + (size_t)comm->slotTotal * kFlagStride;
   dc.unused = nullptr;
   NCCLCHECK(hipErr(hipMalloc(&comm->dComm, sizeof(DevComm)), "hipMalloc devComm"));
   NCCLCHECK(hipErr(hipMemcpy(comm->dComm, &dc, sizeof(dc), hipMemcpyHostToDevice), "hipMemcpy"));

@@ -77,7 +77,7 @@ Knobs Knobs::fromEnv() {
   k.ll128Remote = envInt("MSCCL_AMD_LL128_REMOTE", 0) != 0;
   k.ringOn = listEnables(getenv("NCCL_ALGO"), "Ring", true);
   k.treeOn = listEnables(getenv("NCCL_ALGO"), "Tree", true);
-  k.treeMaxBytes = envInt("MSCCL_AMD_TREE_MAX_BYTES", -1);  // -1: 16 KiB per rank (makeRingPlan)
+  k.treeMaxBytes = envInt("MSCCL_AMD_TREE_MAX_BYTES", -1);  // -1: the defaults of makeRingPlan / makeFlatTreePlan
   k.smallKernel = envInt("MSCCL_AMD_SMALL_KERNEL", 1) != 0;
   k.fuse = envInt("MSCCL_AMD_FUSE", 1) != 0;
   k.treeFlat = envInt("MSCCL_AMD_TREE_FLAT", 1) != 0;

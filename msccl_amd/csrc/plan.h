@@ -68,7 +68,9 @@ struct Knobs {
   int32_t ringFallback;      // MSCCL_AMD_RING_FALLBACK
   int32_t ll128Remote;       // MSCCL_AMD_LL128_REMOTE: allow LL128 towards peers on other GPUs
   int32_t ringOn, treeOn;    // NCCL_ALGO enables Ring / Tree for the fallback (tuning.cc:188-197)
-  int64_t treeMaxBytes;      // MSCCL_AMD_TREE_MAX_BYTES: AllReduce fallback calls up to this size take the tree
+  int64_t treeMaxBytes;      // MSCCL_AMD_TREE_MAX_BYTES: AllReduce fallback calls up to this size take the
+                             // tree (-1: 512 KiB for the flat tree, else 16 KiB per rank); when set it also
+                             // caps a rank's block for the flat ReduceScatter / AllGather
   int32_t smallKernel;       // MSCCL_AMD_SMALL_KERNEL: one-iteration LL launches take mscclSmallKernel
   int32_t referenceSelection;  // MSCCL_AMD_REFERENCE_SELECTION: the reference's MSCCL gating (below)
   int32_t fuse;              // MSCCL_AMD_FUSE: fused s + rrc exchanges (transport.cc: fusableTbs)
@@ -99,8 +101,9 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p);
 //   a tree AllReduce plan (makeRingPlan chose the tree, LL, op Sum..Min, 2..16 ranks): every rank
 //   sends its input to every peer and folds the n inputs in the chain tree's order x_{n-1} (+)
 //   x_{n-2} (+) ... (+) x_0, instead of 2 (n - 1) hops;
-//   an LL ring ReduceScatter (op Sum..Min) or AllGather of at most MSCCL_AMD_TREE_MAX_BYTES per
-//   rank's block (default 16 KiB): every rank sends block p to peer p and folds its own block in
+//   an LL ring ReduceScatter (op Sum..Min) or AllGather (the whole LL range, 512 KiB in all, by
+//   default; MSCCL_AMD_TREE_MAX_BYTES, when set, also caps a rank's block): every rank sends block
+//   p to peer p and folds its own block in
 //   the ring's order x_{r+1} (+) x_{r+2} (+) ... (+) x_{r+n-1} (+) x_r (ReduceScatter), or sends
 //   its block to every peer and stores each peer's at its place (AllGather), instead of n - 1.
 // Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).

@@ -244,26 +244,102 @@ def _slot_of(r: int, p: int) -> int:
     return r if r < p else r - 1
 
 
+def hamiltonian_decomposition(n: int, budget: int = 200000) -> Optional[List[List[int]]]:
+    """n - 1 arc-disjoint directed Hamiltonian cycles of the complete directed graph on n vertices
+    (every ordered pair (i, j), i != j, is an arc of exactly one cycle), or None.  They exist for
+    every n except 4 and 6 (Tillson's theorem); this is a seeded depth-first search, which finds
+    them at once for the node sizes here (n = 8: the first seed, a few thousand steps).  On a fully
+    connected xGMI node every GPU then sends on all n - 1 of its links when the channels' rings
+    are spread over the cycles (the rotations i -> i + s with s coprime to n give only phi(n)
+    of them: 4 of 7 links on 8 GPUs)."""
+    import random
+    if n < 2:
+        return None
+    if n == 2:
+        return [[0, 1]]
+    if n in (4, 6):
+        return None
+    for seed in range(64):
+        rnd = random.Random(seed)
+        used = [[False] * n for _ in range(n)]
+        cycles: List[List[int]] = []
+        steps = [0]
+
+        def cycle(path, inpath):
+            steps[0] += 1
+            if steps[0] > budget:
+                raise TimeoutError
+            u = path[-1]
+            if len(path) == n:
+                if used[u][path[0]]:
+                    return False
+                used[u][path[0]] = True
+                if solve():
+                    return True
+                used[u][path[0]] = False
+                return False
+            cand = [v for v in range(n) if not inpath[v] and not used[u][v]]
+            rnd.shuffle(cand)
+            for v in cand:
+                used[u][v] = inpath[v] = True
+                path.append(v)
+                if cycle(path, inpath):
+                    return True
+                path.pop()
+                used[u][v] = inpath[v] = False
+            return False
+
+        def solve():
+            if len(cycles) == n - 1:
+                return True
+            path, inpath = [0], [False] * n
+            inpath[0] = True
+            cycles.append(path)
+            if cycle(path, inpath):
+                return True
+            cycles.pop()
+            return False
+        try:
+            if solve():
+                return [list(c) for c in cycles]
+        except TimeoutError:
+            continue
+    return None
+
+
+def ring_cycles(n: int, channels: int) -> List[List[int]]:
+    """The ring (a Hamiltonian cycle, as the rank order along it) of every channel: the n - 1
+    arc-disjoint cycles of hamiltonian_decomposition dealt round-robin over the channels, or, where
+    none exists (n = 4, 6), the rotations i -> i + s for s coprime to n."""
+    cyc = hamiltonian_decomposition(n)
+    if cyc is None:
+        cyc = [[(i * s) % n for i in range(n)] for s in range(1, n) if _gcd(s, n) == 1]
+    return [cyc[c % len(cyc)] for c in range(channels)]
+
+
 def allreduce_ring(n: int, channels: int = 1, proto: str = "Simple", inplace: bool = True,
                    min_bytes: Optional[int] = 0, max_bytes: Optional[int] = None,
                    nthreads: Optional[int] = None, strides: Optional[List[int]] = None,
-                   name: str = "allreduce_ring") -> str:
+                   name: str = "allreduce_ring", rings: Optional[List[List[int]]] = None) -> str:
     """Ring AllReduce, one ring per channel: s, rrs x (n-2), rrcs, rcs x (n-2), r.
 
-    Channel c walks the Hamiltonian cycle i -> i + stride_c (mod n); with strides coprime to n
-    (1, 3, 5, 7 on 8 ranks) the channels use disjoint directed xGMI links.
+    Channel c walks rings[c] (the rank order along a Hamiltonian cycle).  Default: ring_cycles,
+    the n - 1 arc-disjoint directed Hamiltonian cycles of the full mesh spread over the channels,
+    so every GPU sends on all its xGMI links; `strides` gives the rotation i -> i + stride_c
+    instead (the round-3 form: with strides coprime to n only phi(n) cycles exist).
     """
-    if strides is None:
-        cands = [s for s in range(1, n) if _gcd(s, n) == 1]
-        strides = [cands[c % len(cands)] for c in range(channels)]
+    if rings is None:
+        if strides is not None:
+            rings = [[(i * st) % n for i in range(n)] for st in strides]
+        else:
+            rings = ring_cycles(n, channels)
     ncpl = channels * n
     gpus = {}
     ob = "i" if inplace else "o"
     for r in range(n):
         tbs = []
         for c in range(channels):
-            st = strides[c]
-            ring = [(i * st) % n for i in range(n)]
+            ring = rings[c]
             pos = ring.index(r)
             nxt = ring[(pos + 1) % n]
             prv = ring[(pos - 1) % n]

@@ -202,3 +202,168 @@ def test_calibrate_xgmi_returns_a_rate():
     gbs = bench.calibrate_xgmi(nbytes=64 << 20, reps=3)
     print("one-way peer copy cuda:0 -> cuda:1: %s GB/s" % gbs)
     assert isinstance(gbs, float) and gbs > 1.0
+
+
+# ------------------------------------------------------------------------------------------------
+# eight devices: BASELINE.json's 8-GPU configs (C3, C4, C5), one rank per GPU.  They run on the
+# first 8-GPU box (the driver's round-end node); on fewer devices they skip with the reason.
+
+needs8 = pytest.mark.skipif("_ndev() < 8", reason="needs eight visible GPUs (C3 / C4 / C5, one rank per GPU)")
+
+
+def _bench():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import bench
+    return bench
+
+
+def _c3_xml(tmp_path, nbytes):
+    b = _bench()
+    tiers = b.make_xmls(8, "LL", 4, str(tmp_path))
+    return open(b.tier_of(tiers, nbytes)[3]).read()
+
+
+@needs8
+@pytest.mark.parametrize("nbytes", [128, 64 << 10, 32 << 20])
+def test_c3_init_all_eight_devices(tmp_path, nbytes):
+    """C3 (8 ranks, LL, fp16) through ncclCommInitAll(0..7) and bench.py's tier schedule of the size:
+    peer pointers over xGMI to all 7 peers, bit-exact against the oracle."""
+    from tests.gpu_harness import run_collective
+    gpu, ora, _ = run_collective(_c3_xml(tmp_path, nbytes), 8, L.ALLREDUCE, nbytes // 2, 6, 0, True, seed=31,
+                                 devices=list(range(8)))
+    _check(gpu, ora, "C3 %d B on 8 devices" % nbytes)
+
+
+@needs8
+def test_c4_init_all_eight_devices():
+    """C4 (8 ranks, ring, Simple, bf16, 32 rings over the 7 Hamiltonian cycles): the oracle at 8 MiB
+    per rank, exact integers at the full 256 MiB (every association order gives the exact sum)."""
+    from tests.gpu_harness import run_collective
+    xml = xmlgen.allreduce_ring(8, 32, "Simple", True, 0, 1 << 40, name="c4_ring")
+    gpu, ora, _ = run_collective(xml, 8, L.ALLREDUCE, (8 << 20) // 2, 9, 0, True, seed=32, devices=list(range(8)))
+    _check(gpu, ora, "C4 8 MiB on 8 devices")
+    gpu, ora, _ = run_collective(xml, 8, L.ALLREDUCE, (256 << 20) // 2, 9, 0, True, seed=33, mode="exact",
+                                 devices=list(range(8)))
+    _check(gpu, ora, "C4 256 MiB exact on 8 devices")
+
+
+@needs8
+def test_c5_init_all_eight_devices():
+    """C5 (8 ranks, fp32, 64 MiB): ReduceScatter (chain form) then AllGather, Simple, each bit-exact."""
+    from tests.gpu_harness import run_collective
+    rc = (64 << 20) // 4 // 8
+    rs = xmlgen.reduce_scatter_allpairs(8, 4, "Simple", False, 0, 1 << 40, name="c5_rs")
+    gpu, ora, _ = run_collective(rs, 8, L.REDUCE_SCATTER, rc, 7, 0, False, seed=34, devices=list(range(8)))
+    _check(gpu, ora, "C5 ReduceScatter on 8 devices")
+    ag = xmlgen.allgather_allpairs(8, 4, "Simple", False, 0, 1 << 40, name="c5_ag")
+    gpu, ora, _ = run_collective(ag, 8, L.ALLGATHER, rc, 7, 0, False, seed=35, devices=list(range(8)))
+    _check(gpu, ora, "C5 AllGather on 8 devices")
+
+
+def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out):
+    """One rank of an 8-process job: every (coll, count, dt, seed) of `jobs` in place (AllReduce)
+    or out of place (RS / AG), results back to the parent."""
+    import torch
+    os.environ["MSCCL_XML_FILES"] = xml_path
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "60"
+    torch.cuda.set_device(rank)
+    uid = M.get_unique_id() if rank == 0 else None
+    if rank == 0:
+        for _ in range(world - 1):
+            q_in.put(uid)
+    else:
+        uid = q_in.get(timeout=120)
+    from tests.gpu_harness import gen_inputs, to_torch
+    comm = M.Comm.init_rank(world, uid, rank)
+    dev = torch.device("cuda", rank)
+    s = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for coll, count, dt, seed in jobs:
+        if coll == L.ALLREDUCE:
+            t = to_torch(gen_inputs(world, count, dt, seed)[rank], dev)
+            comm.all_reduce(t.data_ptr(), t.data_ptr(), count, dt, M.SUM, s)
+        elif coll == L.REDUCE_SCATTER:
+            x = to_torch(gen_inputs(world, count * world, dt, seed)[rank], dev)
+            t = torch.zeros(count, dtype=x.dtype, device=dev)
+            comm.reduce_scatter(x.data_ptr(), t.data_ptr(), count, dt, M.SUM, s)
+        else:
+            x = to_torch(gen_inputs(world, count, dt, seed)[rank], dev)
+            t = torch.zeros(count * world, dtype=x.dtype, device=dev)
+            comm.all_gather(x.data_ptr(), t.data_ptr(), count, dt, s)
+        torch.cuda.synchronize()
+        outs.append(t.cpu().numpy())
+    err = comm.async_error()
+    comm.destroy()
+    q_out.put((rank, err, outs))
+
+
+def _eight_processes(tmp_path, xmls, jobs):
+    import torch.multiprocessing as mp
+    world = 8
+    paths = []
+    for i, x in enumerate(xmls):
+        p = tmp_path / ("s%d.xml" % i)
+        p.write_text(x)
+        paths.append(str(p))
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_rank_proc8, args=(r, world, ":".join(paths), jobs, q_in, q_out)) for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, outs = q_out.get(timeout=600)
+        res[r] = (err, outs)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    return res
+
+
+def _oracle(xmls, coll, count, dt, seed, in_place):
+    """The oracle's outputs of one call of the 8-rank job (the schedule the reference's selection
+    picks among xmls, tests/gpu_harness.py: CoResident.oracle without a GPU)."""
+    import types
+    from tests.gpu_harness import CoResident, gen_inputs
+    world = 8
+    fake = types.SimpleNamespace(n=world, algos=[[L.parse_xml(x, r, world) for x in xmls] for r in range(world)])
+    n_in = count * world if coll == L.REDUCE_SCATTER else count
+    outs, _ = CoResident.oracle(fake, coll, count, dt, 0, gen_inputs(world, n_in, dt, seed), in_place)
+    return outs
+
+
+@needs8
+def test_eight_processes_c3_c5_ipc(tmp_path):
+    """One process per GPU (the reference's mpirun -np 8 -g 1, README.md:57): hipIpc FIFOs between
+    all 8 GPUs, C3's tiers at 128 B / 64 KiB / 32 MiB, then C5's ReduceScatter and AllGather, every
+    rank bit-exact against the oracle."""
+    b = _bench()
+    tiers = b.make_xmls(8, "LL", 4, str(tmp_path))
+    c3 = [open(t[3]).read() for t in tiers]
+    rc = (64 << 20) // 4 // 8
+    c5 = [xmlgen.reduce_scatter_allpairs(8, 4, "Simple", False, 0, 1 << 40, name="c5_rs"),
+          xmlgen.allgather_allpairs(8, 4, "Simple", False, 0, 1 << 40, name="c5_ag")]
+    jobs = [(L.ALLREDUCE, nb // 2, 6, 40 + k) for k, nb in enumerate((128, 64 << 10, 32 << 20))]
+    jobs += [(L.REDUCE_SCATTER, rc, 7, 50), (L.ALLGATHER, rc, 7, 51)]
+    res = _eight_processes(tmp_path, c3 + c5, jobs)
+    for j, (coll, count, dt, seed) in enumerate(jobs):
+        xs = c3 if coll == L.ALLREDUCE else c5
+        want = _oracle(xs, coll, count, dt, seed, coll == L.ALLREDUCE)
+        for r in range(8):
+            assert res[r][0] == 0
+            _check([res[r][1][j]], [want[r]], "8 processes job %d rank %d" % (j, r))
+
+
+@needs8
+def test_eight_processes_c4_ipc(tmp_path):
+    """C4 one rank per GPU: the 32-ring Simple bf16 schedule at 8 MiB per rank against the oracle."""
+    xml = xmlgen.allreduce_ring(8, 32, "Simple", True, 0, 1 << 40, name="c4_ring")
+    jobs = [(L.ALLREDUCE, (8 << 20) // 2, 9, 60)]
+    res = _eight_processes(tmp_path, [xml], jobs)
+    want = _oracle([xml], L.ALLREDUCE, (8 << 20) // 2, 9, 60, True)
+    for r in range(8):
+        assert res[r][0] == 0
+        _check([res[r][1][0]], [want[r]], "C4 8 processes rank %d" % r)

@@ -116,3 +116,34 @@ def test_npkit_off_by_default(tmp_path):
     with CoResident(2, [xml], str(tmp_path)) as cr:
         with pytest.raises(M.NcclError):
             cr.comms[0].npkit_dump(str(tmp_path / "x"))
+
+
+def test_npkit_and_trace_cover_the_fold_kernel(tmp_path, monkeypatch):
+    """A fallback call that runs the flat fold kernel (no schedule loaded, the flat tree) still
+    logs: per launch TIME_SYNC_CPU / TIME_SYNC_GPU and its one pass as RECV_REDUCE_COPY_SEND with
+    the call's bytes in thread block 0's buffer; MSCCL_AMD_TRACE=1 records the workgroup's setup,
+    primitive begin / end and end events."""
+    import torch
+    n, launches, count, dt = 2, 3, 1000, 7
+    monkeypatch.setenv("NCCL_ALGO", "Ring,Tree")
+    monkeypatch.setenv("MSCCL_AMD_NPKIT", "1")
+    monkeypatch.setenv("MSCCL_AMD_NPKIT_EVENTS", "64")
+    monkeypatch.setenv("MSCCL_AMD_TRACE", "1")
+    with CoResident(n, [], str(tmp_path)) as cr:
+        t = [to_torch(x, torch.device("cuda:0")) for x in gen_inputs(n, count, dt, 5)]
+        p = [x.data_ptr() for x in t]
+        for _ in range(launches):
+            cr.run(L.ALLREDUCE, count, dt, 0, p, p)
+        last = cr.comms[0].info()["last"]
+        assert last["ringColl"] == 5 and last["small"] == 2, last
+        tr = cr.comms[0].trace()
+        cr.comms[0].npkit_dump(str(tmp_path / "fold"))
+    hdr = tr[0, 0]
+    assert hdr["type"] == 0xFFFF and hdr["step"] == 5
+    assert [M.TRACE_TYPES.get(int(e["type"])) for e in tr[0, 1:5]] == [M.TRACE_TYPES[k] for k in (1, 3, 4, 5)]
+    ev = npkit.read_buffer(str(tmp_path / "fold"), 0, 0)
+    got = [(npkit.NAMES[e["id"]], e["size"]) for e in ev]
+    want = [("NPKIT_EVENT_TIME_SYNC_CPU", 0), ("NPKIT_EVENT_TIME_SYNC_GPU", 0),
+            ("NPKIT_EVENT_RECV_REDUCE_COPY_SEND_ENTRY", count * 4),
+            ("NPKIT_EVENT_RECV_REDUCE_COPY_SEND_EXIT", count * 4)] * launches
+    assert got == want

@@ -207,7 +207,9 @@ def test_tree_threshold_and_repeats(monkeypatch):
 def _flat_env(monkeypatch, tree_max=None):
     monkeypatch.setenv("NCCL_ALGO", "Ring,Tree")
     if tree_max is None:
-        monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES")   # default 16 KiB x n per rank
+        # defaults: AllReduce up to 512 KiB on the flat tree; flat ReduceScatter / AllGather over
+        # the whole LL range (512 KiB in all), no per-block cap
+        monkeypatch.delenv("MSCCL_AMD_TREE_MAX_BYTES", raising=False)
     else:
         monkeypatch.setenv("MSCCL_AMD_TREE_MAX_BYTES", str(tree_max))
 
@@ -262,7 +264,8 @@ def test_flat_tree_across_ll_cleanup(monkeypatch):
 @pytest.mark.parametrize("count", [1, 37, 512, 4095])
 @pytest.mark.parametrize("in_place", [True, False])
 def test_flat_reduce_scatter_equals_the_ring(monkeypatch, n, count, in_place):
-    """LL ReduceScatters of at most 16 KiB per rank's block take the fold kernel's one hop: block
+    """LL ReduceScatters in the LL range (no per-block cap by default; MSCCL_AMD_TREE_MAX_BYTES caps a
+    rank's block when set) take the fold kernel's one hop: block
     p to peer p, the own block folded in the ring's order x_{r+1} (+) ... (+) x_{r+n-1} (+) x_r;
     the oracle is oracle/ring.py's ring (reduce_scatter.h:13-67), bit for bit."""
     _flat_env(monkeypatch)
@@ -274,7 +277,8 @@ def test_flat_reduce_scatter_equals_the_ring(monkeypatch, n, count, in_place):
 @pytest.mark.parametrize("count", [1, 37, 512, 8191])
 @pytest.mark.parametrize("in_place", [True, False])
 def test_flat_all_gather_equals_the_ring(monkeypatch, n, count, in_place):
-    """LL AllGathers of at most 16 KiB per rank take the fold kernel: every rank's block to every
+    """LL AllGathers in the LL range (no per-block cap by default) take the fold kernel: every rank's
+    block to every
     peer, each stored at its place (all_gather.h:13-78's result)."""
     _flat_env(monkeypatch)
     rp = check(n, L.ALLGATHER, count, 6, in_place=in_place, seed=9 + n)

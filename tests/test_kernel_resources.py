@@ -59,3 +59,69 @@ def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
     assert len(small) == 3 * 4 * 2, sorted(small)
     for k, v in small.items():
         assert v.get("scratch", 1) == 0, (k, v)
+
+
+# ---------------------------------------------------------------------------------------------
+# Inline asm that issues a vector- or scalar-memory instruction takes VGPR inputs only.  The
+# compiler's hazard recognizer does not insert the "VALU writes an SGPR, VMEM reads it" wait states
+# for operands of inline asm: a wave-uniform slot base moved to an SGPR with v_readfirstlane two
+# instructions before a global_load's `saddr` operand was read stale, which hung one run and
+# faulted the next with an illegal memory access (commit 30ad87d).
+DEVICE = os.path.join(ROOT, "msccl_amd", "csrc", "device")
+MEM_INSN = re.compile(r"\b(global_|buffer_|flat_|scratch_|s_load|s_buffer_load|s_store|s_buffer_store|s_dcache)")
+ALLOWED_INPUT = re.compile(r'^"[vin]"$')
+
+
+def _asm_blocks(text):
+    """(template, inputs) of every asm statement: the parenthesised body split at top-level colons."""
+    out = []
+    for m in re.finditer(r"\basm\s*(volatile\s*)?\(", text):
+        i, depth, parts, cur, instr = m.end(), 1, [], [], False
+        while i < len(text) and depth:
+            ch = text[i]
+            if ch == '"' and text[i - 1] != "\\":
+                instr = not instr
+            if not instr:
+                if ch == "(":
+                    depth += 1
+                elif ch == ")":
+                    depth -= 1
+                    if depth == 0:
+                        break
+                elif ch == ":" and depth == 1:
+                    parts.append("".join(cur))
+                    cur = []
+                    i += 1
+                    continue
+            cur.append(ch)
+            i += 1
+        parts.append("".join(cur))
+        template = parts[0]
+        inputs = parts[2] if len(parts) > 2 else ""
+        out.append((template, re.findall(r'("[^"]*")\s*\(', inputs)))
+    return out
+
+
+def _bad_asm(text):
+    return [(t.strip()[:60], c) for t, cons in _asm_blocks(text) if MEM_INSN.search(t)
+            for c in cons if not ALLOWED_INPUT.match(c)]
+
+
+def test_memory_asm_takes_vgpr_operands_only():
+    srcs = glob.glob(os.path.join(DEVICE, "*.h")) + glob.glob(os.path.join(DEVICE, "*.hip"))
+    assert srcs
+    n = 0
+    for f in srcs:
+        text = open(f).read()
+        n += sum(1 for t, _ in _asm_blocks(text) if MEM_INSN.search(t))
+        assert _bad_asm(text) == [], f
+    assert n >= 5   # the FIFO line polls (primitives.h: ldLines*) are found
+
+
+def test_memory_asm_check_catches_an_sgpr_operand():
+    ok = 'asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\\n\\ts_waitcnt vmcnt(0)" : "=&v"(x) : "v"(a) : "memory");'
+    bad = ('asm volatile("global_load_dwordx4 %0, %1, %2 sc0 sc1\\n\\ts_waitcnt vmcnt(0)" : "=&v"(x) '
+           ': "v"(off), "s"(base) : "memory");')
+    reg = 'asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));'
+    assert _bad_asm(ok) == [] and _bad_asm(reg) == []
+    assert [c for _, c in _bad_asm(bad)] == ['"s"']

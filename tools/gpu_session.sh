@@ -1,0 +1,70 @@
+#!/bin/bash
+# One GPU session, run from the repo root on the GPU box: the steps named in STEPS, outputs under
+# gpurun_out/$TAG_*.  Every GPU step runs under its own time limit and the first failure ends the
+# session (nothing more touches the GPU after a fault, an abort or a time limit).
+#   suite     the GPU test suite (pytest -m gpu)
+#   lat       graph-replay latency per launch (tools/lat_one.py) of every library in LIBS on the
+#             2-rank pair tier, the 8-rank C3 small tier and the flat fold, same box
+#   trace     tools/lat_trace.py on LATLIB (a MSCCL_LAT_TRACE build, see msccl_amd/csrc/Makefile)
+#   bench     the default bench line (N=1, C2, live PMC)
+#   c345      the 8-rank C3 shape plus C4 / C5 (co-resident ranks)
+#   spawn     the 2-process launcher rehearsal on one GPU and the launcher's refusal
+#   sweep     bench.py sweeps of every library in LIBS (C2 2 ranks, then C3 shape 8 ranks fp16)
+# e.g. STEPS="suite lat" LIBS="tools/ab/a.so msccl_amd/libmsccl_amd.so" TAG=r04a bash tools/gpu_session.sh
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${TAG:-r04}
+STEPS=${STEPS:-"suite bench"}
+LIBS=${LIBS:-msccl_amd/libmsccl_amd.so}
+O=gpurun_out/$TAG
+mkdir -p gpurun_out
+fail() { echo "FAILED: $*"; [ -n "$2" ] && tail -30 "$2"; exit 1; }
+lat() { timeout -k 5 90 python3 tools/lat_one.py --iters 300 --graph "$@" 2>&1 | grep -v amdgpu.ids; }
+for step in $STEPS; do
+  case $step in
+  suite)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+      > ${O}_suite.txt 2>&1 || fail suite ${O}_suite.txt
+    tail -2 ${O}_suite.txt ;;
+  lat)
+    for L in $LIBS; do
+      for spec in "pair 128 2 1 7" "pair 4096 2 16 7" "pair 65536 2 16 7" "oneshot 128 8 4 6" "oneshot 4096 8 4 6" \
+                  "fbtree 128 2 1 7" "fbtree 128 8 1 6"; do
+        set -- $spec
+        r=$(MSCCL_AMD_LIB=$L lat --schedule $1 --bytes $2 --ranks $3 --instances $4 --dtype $5) || fail "lat $L $spec"
+        echo "$(basename $L) $r" | tee -a ${O}_lat.txt
+      done
+    done ;;
+  trace)
+    MSCCL_AMD_LIB=${LATLIB:-tools/ab/libmsccl_amd_lat.so} MSCCL_AMD_TRACE=2 timeout -k 5 90 python3 tools/lat_trace.py \
+      > ${O}_trace.txt 2>&1 || fail trace ${O}_trace.txt
+    cat ${O}_trace.txt ;;
+  bench)
+    timeout -k 10 400 python3 bench.py > ${O}_bench.json 2> ${O}_bench.err || fail bench ${O}_bench.err
+    python3 -c "import json; d=json.load(open('${O}_bench.json')); print('bench', d['value'], d['avg_busbw'], d['roofline']['frac'], d['roofline'].get('traffic_over_algorithmic'))" ;;
+  c345)
+    timeout -k 10 400 python3 bench.py --vranks 8 --dtype fp16 --sizes 128,65536,33554432 --extras C4,C5 --no-cpu --pmc off \
+      --no-secondary > ${O}_c345_8.json 2> ${O}_c345_8.err || fail c345 ${O}_c345_8.err ;;
+  spawn)
+    MSCCL_AMD_BENCH_ONE_GPU=1 timeout -k 10 300 python3 bench.py --gpus 2 --no-cpu --pmc off \
+      > ${O}_spawn2.json 2> ${O}_spawn2.err || fail spawn ${O}_spawn2.err
+    timeout -k 10 120 python3 bench.py --gpus 2 > ${O}_refuse2.json 2> ${O}_refuse2.err
+    echo "refuse rc=$?" | tee ${O}_refuse2.rc ;;
+  sweep)
+    for L in $LIBS; do
+      b=$(basename $L .so)
+      MSCCL_AMD_LIB=$L timeout -k 10 300 python3 bench.py --no-cpu --pmc off --no-secondary \
+        > ${O}_sweep2_$b.json 2>> ${O}_sweep.err || fail "sweep2 $L" ${O}_sweep.err
+      MSCCL_AMD_LIB=$L timeout -k 10 300 python3 bench.py --vranks 8 --dtype fp16 --no-cpu --pmc off --no-secondary \
+        > ${O}_sweep8_$b.json 2>> ${O}_sweep.err || fail "sweep8 $L" ${O}_sweep.err
+      python3 -c "
+import json
+for k in ('2', '8'):
+    d = json.load(open('${O}_sweep%s_$b.json' % k))
+    print('$b', k, 'ranks: value %.1f avg %.1f |' % (d['value'], d['avg_busbw']), ' '.join('%d:%.2f' % (s['bytes'], s['ms'] * 1e3) for s in d['sweep']))
+" | tee -a ${O}_sweep.txt
+    done ;;
+  *) fail "unknown step $step" ;;
+  esac
+done
+echo "session done"
