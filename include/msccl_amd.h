@@ -25,6 +25,12 @@ int mscclAmdAlgoJson(const char* xmlPath, int rank, int nranks, char* out, size_
  * channel, peer], ...]}.  No GPU needed. */
 int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, size_t outLen);
 
+/* Whether the AllReduce schedule of one MSCCL XML file, loaded for every rank of `nranks`, runs as
+ * the one-hop fold (msccl_amd/csrc/lower.cc: every result chunk of every rank is a left fold of all
+ * ranks' same chunk in one order per rank).  JSON {"ok":1,"order":[[ranks of rank 0's fold], ...]}
+ * or {"ok":0,"why":"..."}.  No GPU needed. */
+int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen);
+
 /* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the launch plan
  * (enqueue.cc:591-734).  coll uses ncclFunc_t numbering (AllGather=2, ReduceScatter=3,
  * AllReduce=4).  Writes JSON {"algo":i,...} or {"algo":-1}.  No GPU needed. */

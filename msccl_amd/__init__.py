@@ -86,6 +86,8 @@ def lib() -> ctypes.CDLL:
     L.ncclGroupEnd.argtypes = []
     L.mscclAmdAlgoJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
     L.mscclAmdFusableJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
+    if hasattr(L, "mscclAmdLowerJson"):  # MSCCL_AMD_LIB may name an older build (A/B runs)
+        L.mscclAmdLowerJson.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, sz]
     L.mscclAmdPlanJson.argtypes = [ctypes.c_char_p, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
     L.mscclAmdCommInfo.argtypes = [vp, ctypes.c_char_p, sz]
     L.mscclAmdNpkitDump.argtypes = [vp, ctypes.c_char_p]
@@ -145,6 +147,14 @@ def fusable_json(xml_path: str, rank: int, nranks: int, key: str = "fusable") ->
     buf = ctypes.create_string_buffer(1 << 20)
     _check(lib().mscclAmdFusableJson(xml_path.encode(), rank, nranks, buf, len(buf)), "mscclAmdFusableJson")
     return json.loads(buf.value.decode())[key]
+
+
+def lower_json(xml_path: str, nranks: int) -> dict:
+    """Whether the AllReduce schedule runs as the one-hop fold kernel (msccl_amd/csrc/lower.cc):
+    {"ok": 1, "order": [fold order of rank 0, ...]} or {"ok": 0, "why": reason}."""
+    buf = ctypes.create_string_buffer(1 << 16)
+    _check(lib().mscclAmdLowerJson(xml_path.encode(), nranks, buf, len(buf)), "mscclAmdLowerJson")
+    return json.loads(buf.value.decode())
 
 
 def line_tear_probe(writer_dev: int, reader_dev: int, lines: int = 1 << 16, iters: int = 2000,

@@ -71,6 +71,10 @@ struct ncclComm {
   std::vector<msccl::Algorithm> algos;
   std::vector<msccl::Registration> regs;
   std::vector<msccl::DevAlgoHost> devAlgos;
+  // per algorithm: this rank's fold order when the schedule runs as the one-hop fold (lower.cc;
+  // empty: it does not) and the fold kernel's program for it (nBlocks 0 when empty)
+  std::vector<std::vector<int>> algoFoldOrder;
+  std::vector<msccl::DevAlgoHost> foldAlgos;
   msccl::DevAlgoHost ringAlgos[6];  // ring fallback programs, [4] = tree, [5] = flat tree (transport.cc: ringUpload)
   msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank
   bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank

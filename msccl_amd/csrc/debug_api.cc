@@ -12,6 +12,7 @@
 #include "bootstrap.h"
 #include "comm.h"
 #include "debug.h"
+#include "lower.h"
 #include "plan.h"
 
 using namespace msccl;
@@ -50,6 +51,31 @@ int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, si
         first = false;
       }
   o << "]}";
+  return putOut(o.str(), out, outLen);
+}
+
+int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen) {
+  if (!xmlPath || nranks < 1) return ncclInvalidArgument;
+  std::vector<Algorithm> byRank(nranks);
+  for (int r = 0; r < nranks; r++) {
+    const int res = loadAlgoFromXml(xmlPath, &byRank[r], kMaxChannels, r, nranks);
+    if (res != 0) return res;
+  }
+  const FoldLowering fl = analyzeFoldLowering(byRank);
+  std::ostringstream o;
+  o << "{\"ok\":" << (fl.ok ? 1 : 0);
+  if (fl.ok) {
+    o << ",\"order\":[";
+    for (size_t r = 0; r < fl.order.size(); r++) {
+      o << (r ? "," : "") << "[";
+      for (size_t i = 0; i < fl.order[r].size(); i++) o << (i ? "," : "") << fl.order[r][i];
+      o << "]";
+    }
+    o << "]";
+  } else {
+    o << ",\"why\":\"" << fl.why << "\"";
+  }
+  o << "}";
   return putOut(o.str(), out, outLen);
 }
 

@@ -48,7 +48,7 @@ enum TraceType : uint16_t {
   kEvSetup = 1,      // program staged, connections read
   kEvDepWait = 2,    // dependency flags satisfied (step = transfer index)
   kEvPrimBegin = 3,  // arg = transfer type << 24 | elements of this workgroup (capped)
-  kEvPrimEnd = 4,
+  kEvPrimEnd = 4,    // arg = 10-ns ticks waited for the Simple tail << 16 | ticks waited for send credit
   kEvEnd = 5,        // workgroup done
   kEvHeader = 0xFFFF
 };

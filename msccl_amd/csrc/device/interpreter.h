@@ -41,6 +41,9 @@ struct alignas(16) BlockShared {
   uint64_t seen[2];        // send head / recv tail last observed
   uint64_t epoch;
   uint32_t aborted;
+  // MSCCL_AMD_TRACE=1: 10-ns ticks the polling lane spent waiting in this primitive call for the
+  // Simple tail (data) and for send credit (head), saturating; in the padding of the struct
+  uint16_t waitTail, waitHead;
 };
 
 // The flat tree's fold kernel (Interp::runFold), besides BlockShared: per peer, its send and recv
@@ -203,6 +206,11 @@ struct Interp {
     return false;
   }
 
+  static __device__ __forceinline__ uint16_t addTicks(uint16_t acc, uint64_t since) {
+    const uint64_t d = acc + (__builtin_amdgcn_s_memrealtime() - since);
+    return (uint16_t)(d > 0xFFFF ? 0xFFFF : d);
+  }
+
   // Send credit: the receiver has freed slot `sendStep` once head + SLOTS > sendStep.  The
   // last head seen is kept (and persisted in the connection), so most steps need no poll of the
   // remote word, whose round trip is the largest part of a small message's latency.
@@ -212,9 +220,11 @@ struct Interp {
     if (tid == 0) {
       Spin spins;
       uint64_t h;
+      const uint64_t tw = trace != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
       while ((h = atomicLoadSys(sc->head)) + SLOTS < sendStep + 1) {
         if (spinAbort(spins)) break;
       }
+      if (trace != nullptr) sh->waitHead = addTicks(sh->waitHead, tw);
       sh->seen[0] = h;
     }
     __syncthreads();
@@ -238,9 +248,11 @@ struct Interp {
     if (tid == 0) {
       Spin spins;
       uint64_t t;
+      const uint64_t tw = trace != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
       while ((t = atomicLoadSys(rc->tail)) < recvStep + 1) {
         if (spinAbort(spins)) break;
       }
+      if (trace != nullptr) sh->waitTail = addTicks(sh->waitTail, tw);
       if (rc->remote == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       else if (rc->remote == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       sh->seen[1] = t;
@@ -1265,6 +1277,7 @@ struct Interp {
             s.Lq = q1 - q0;
             s.npk = thisCount * s.Lq;
           }
+          if (trace != nullptr && tid == 0) sh->waitTail = sh->waitHead = 0;
           ev(kEvPrimBegin, (uint16_t)i, ((uint32_t)t.type << 24) | (uint32_t)min(s.npk * PE, 0xFFFFFF));
           nk(nkPrim(t.type), (uint64_t)s.n * TS);
           if (!exec<false>(t, srcP, dstP, srcoff, dstoff, grid + (int64_t)c * sizePer, sizePer, s)) {
@@ -1273,7 +1286,8 @@ struct Interp {
           }
           nk(nkPrim(t.type) + 1, (uint64_t)s.n * TS);
           if (t.type == tRe && c == 0) step += t.numReds - 1;
-          ev(kEvPrimEnd, (uint16_t)i, 0);
+          // arg: ticks waited for the Simple tail (high half) and for send credit (low half)
+          ev(kEvPrimEnd, (uint16_t)i, trace != nullptr && tid == 0 ? ((uint32_t)sh->waitTail << 16) | sh->waitHead : 0);
         }
         if (stop) break;
         if (fused || sendCpy) {  // the s published nothing (transport.cc); the second transfer's flag below

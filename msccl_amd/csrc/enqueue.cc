@@ -122,6 +122,12 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
     protoOverride = kProtoLL;
   }
   NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, comm->knobs, &out->plan));
+  if ((size_t)idx < comm->algoFoldOrder.size() && !comm->algoFoldOrder[idx].empty() && flatEnabled(comm) &&
+      lowerToFoldPlan(c, comm->knobs, &out->plan) == 0) {
+    // a one-hop schedule (lower.cc): the fold kernel computes its values in one hop
+    INFO(kSubColl, "MSCCL: %s count=%zu runs as the one-hop fold", comm->algos[idx].name.c_str(), op.count);
+    return ncclSuccess;
+  }
   if (out->plan.scratchNeeded > comm->scratchSize) {
     // The scratch is sized from the XMLs' maxBytes at init (init.cc:809-835), so this only
     // happens when MSCCL_AMD_MAX_SCRATCH capped it.  The reference reports ncclInternalError
@@ -185,11 +191,13 @@ RankWork makeRingWork(Planned& p) {
   return w;
 }
 
-// Flat tree (plan.cc: makeFlatTreePlan): the program of transport.cc's ringUpload (ringAlgos[5])
-// run as an MSCCL schedule (ringColl 0 on the device), so one-iteration calls take the small kernel.
+// The fold kernel (interpreter.h: runFold): the flat forms of the fallback (plan.cc:
+// makeFlatTreePlan; transport.cc: ringUpload, ringAlgos[5]) or a lowered one-hop MSCCL schedule
+// (lower.cc; its own fold order, foldAlgos[algoIndex]), over the flat connections.
 RankWork makeFlatWork(Planned& p) {
   ncclComm* comm = p.op.comm;
-  const DevAlgoHost& da = comm->ringAlgos[5];
+  const int lowered = p.plan.algoIndex;  // -1: the fallback's flat forms
+  const DevAlgoHost& da = lowered >= 0 ? comm->foldAlgos[lowered] : comm->ringAlgos[5];
   RankWork w;
   memset(&w, 0, sizeof(w));
   w.sendbuff = p.op.sendbuff;
@@ -235,7 +243,7 @@ RankWork makeFlatWork(Planned& p) {
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.launchSeq = comm->workIndex++;
-  comm->last = {-1, p.plan.proto, wgs, merge, kTreeFlat, 0, w.nBlocks};
+  comm->last = {lowered, p.plan.proto, wgs, merge, kTreeFlat, 0, w.nBlocks};
   return w;
 }
 

@@ -14,6 +14,7 @@
 #include "bootstrap.h"
 #include "comm.h"
 #include "debug.h"
+#include "lower.h"
 #include "group.h"
 #include "plan.h"
 
@@ -40,6 +41,30 @@ ncclResult_t loadAlgos(ncclComm* comm) {
   return ncclSuccess;
 }
 
+// One-hop AllReduce schedules (lower.cc): every rank loads each LL AllReduce schedule once per
+// rank of the communicator (as each of them loads it) and decides the same; the init allgather
+// then keeps a lowering only where every rank reached it (applySplits).
+void analyzeLowering(ncclComm* comm) {
+  comm->algoFoldOrder.assign(comm->algos.size(), {});
+  if (!comm->knobs.lower || !flatEnabled(comm)) return;
+  for (size_t g = 0; g < comm->algos.size(); g++) {
+    const Algorithm& a = comm->algos[g];
+    if (!a.valid || a.coll != kAllReduce || a.proto != kProtoLL || a.path.empty()) continue;
+    std::vector<Algorithm> byRank(comm->nRanks);
+    bool loaded = true;
+    for (int r = 0; r < comm->nRanks && loaded; r++) {
+      if (r == comm->rank) byRank[r] = a;
+      else loaded = loadAlgoFromXml(a.path.c_str(), &byRank[r], kMaxChannels, r, comm->nRanks) == 0;
+    }
+    if (!loaded) continue;
+    const FoldLowering fl = analyzeFoldLowering(byRank);
+    if (fl.ok) comm->algoFoldOrder[g] = fl.order[comm->rank];
+    INFO(kSubInit, "MSCCL: algorithm %s %s", a.name.c_str(),
+         fl.ok ? "is a one-hop fold: calls up to MSCCL_AMD_LOWER_MAX_BYTES run the fold kernel"
+               : ("runs interpreted (" + fl.why + ")").c_str());
+  }
+}
+
 // Per-rank device state that does not depend on peers.
 ncclResult_t commLocalSetup(ncclComm* comm) {
   NCCLCHECK(hipErr(hipSetDevice(comm->cudaDev), "hipSetDevice"));
@@ -53,6 +78,7 @@ ncclResult_t commLocalSetup(ncclComm* comm) {
   }
   comm->knobs = Knobs::fromEnv();
   comm->ringFallback = comm->knobs.ringFallback != 0;
+  analyzeLowering(comm);
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   NCCLCHECK(hipErr(hipHostMalloc((void**)&comm->hostErr, 64, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
   *comm->hostAbort = 0;
@@ -94,6 +120,7 @@ struct SplitRecord {
   int32_t sendRun[kMaxAlgos];
   int32_t nFuse[kMaxAlgos];
   int16_t fuse[kMaxAlgos][kMaxFuse][2];  // (channel, peer) of each fusable exchange (fusableTbs)
+  uint8_t lowered[kMaxAlgos];             // analyzeLowering found the schedule a one-hop fold
   Knobs knobs;
 };
 
@@ -107,6 +134,7 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) {
     s.nBlocks[a] = comm->algos[a].nBlocks;
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
+    s.lowered[a] = a < comm->algoFoldOrder.size() && !comm->algoFoldOrder[a].empty();
     const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
     for (size_t i = 0; i < fc.size() && s.nFuse[a] < kMaxFuse; i++) {
       s.fuse[a][s.nFuse[a]][0] = fc[i].chan;
@@ -143,6 +171,8 @@ static std::string knobDiff(const Knobs& a, const Knobs& b) {
   add(a.referenceSelection != b.referenceSelection, "MSCCL_AMD_REFERENCE_SELECTION");
   add(a.fuse != b.fuse, "MSCCL_AMD_FUSE");
   add(a.treeFlat != b.treeFlat, "MSCCL_AMD_TREE_FLAT");
+  add(a.lower != b.lower, "MSCCL_AMD_LOWER");
+  add(a.lowerMaxBytes != b.lowerMaxBytes, "MSCCL_AMD_LOWER_MAX_BYTES");
   return out.empty() ? "(unnamed field)" : out;
 }
 
@@ -184,6 +214,11 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
   }
+  // a schedule runs as the fold only when every rank found it one (the two ends of every flat
+  // connection must run the same kernel)
+  for (size_t a = 0; a < comm->algoFoldOrder.size() && a < (size_t)kMaxAlgos; a++)
+    for (auto& r : recs)
+      if ((int)a >= r.nAlgos || !r.lowered[a]) comm->algoFoldOrder[a].clear();
   // an exchange runs fused only when both ends offered it (fusableTbs)
   comm->algoFuse.assign(comm->algos.size(), {});
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos && comm->knobs.fuse; a++) {
@@ -218,6 +253,7 @@ static ncclResult_t allocSlots(ncclComm* comm) {
   for (DevAlgoHost& d : comm->devAlgos) take(d, std::max(1, d.nBlocks) * comm->maxSplit);
   for (int k = 0; k < 5; k++) take(comm->ringAlgos[k], std::max(1, comm->ringAlgos[k].nBlocks) * comm->maxSplit);
   take(comm->ringAlgos[5], kFlatSubs);
+  for (DevAlgoHost& d : comm->foldAlgos) take(d, kFlatSubs);  // lowered schedules (lower.cc)
   comm->slotTotal = total;
   const size_t flagWords = (size_t)total * kFlagStride + total;
   NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, flagWords * sizeof(uint64_t)), "hipMalloc flags"));
@@ -345,6 +381,8 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
   }
   for (auto& d : comm->ringAlgos)
     if (d.dImages) hipFree(d.dImages);  // their connection records are comm->ringSend / ringRecv
+  for (auto& d : comm->foldAlgos)
+    if (d.dImages) hipFree(d.dImages);  // the flat connections (comm->flatSend / flatRecv)
   if (comm->ringSend) hipFree(comm->ringSend);
   if (comm->ringRecv) hipFree(comm->ringRecv);
   if (comm->treeSend) hipFree(comm->treeSend);

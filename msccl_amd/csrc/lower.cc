@@ -1,0 +1,272 @@
+// Lowering of one-hop MSCCL AllReduce schedules to the flat fold (interpreter.h: runFold).
+//
+// An msccl-tools schedule is a dataflow program: every rank's thread blocks move chunks through
+// per-(channel, peer) FIFOs and fold them with the reduction op (the reference interprets it
+// step by step: msccl_interpreter.h:66-205).  For small calls the interpretation, not the bytes,
+// is the cost: a one-shot schedule waits on a receive, publishes a flag, wakes a reduce thread
+// block that re-reads the received copies from scratch and copies the result back.  When the
+// program's RESULT on every rank is, for every chunk c, a left fold of all ranks' input chunk c
+// in one fixed order per rank,
+//     out_r[c] = x_{o_r(0)}[c] (+) x_{o_r(1)}[c] (+) ... (+) x_{o_r(n-1)}[c],
+// the same values come out of one hop: every rank sends its input to every peer and folds the
+// n inputs in the order o_r (the flat tree's fold kernel, with o_r as its order table).
+//
+// This file decides that, symbolically: it runs every rank's program (the XML loaded once per
+// rank, as each rank loads it) on chunk-level expressions instead of data, with the reference's
+// semantics for the LL protocol:
+//   s / r / rcs            move values through the (channel, sender, receiver) FIFO, in order;
+//   rrs / rrc / rrcs       fn(peer, local)                               (prims_ll.h:282-287)
+//   re                     acc = d; acc = fn(acc, s_i) in reduction-table order
+//                          (prims_ll.h:347-362; the small path o = fn(s_i, o),
+//                          msccl_interpreter.h:157-170, is the same fold)
+//   cpy                    copy
+//   dependencies           (tb, step) is satisfied once tb published a flag >= step
+//                          (msccl_interpreter.h:121-140,198-201), steps counted as the
+//                          interpreter counts them (fused deps and reductions advance the count)
+//   ra / unknown types     not lowered (the reference ends the thread block there)
+// Expressions are hash-consed with fn(a, b) == fn(b, a): every op the lowering admits (Sum, Prod,
+// Max, Min) is commutative per element in this runtime's arithmetic (IEEE add / mul, the fp16
+// clamp, bf16 RNE of the exact result, integer wrap; the flat tree rests on the same fact,
+// DESIGN.md §8), so a rank's result is then bit for bit the fold kernel's.  Anything else (a
+// schedule that deadlocks, leaves FIFO messages, reads an uninitialised chunk into the result,
+// folds chunks in a tree shape or in orders that differ between chunks of one rank) is not
+// lowered.
+#include <algorithm>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "comm.h"
+#include "lower.h"
+
+namespace msccl {
+
+namespace {
+
+struct Expr {
+  int a, b;  // children (a < b) of fn; leaves have a = -1 and b = rank * nChunks + chunk
+};
+
+class Exprs {
+ public:
+  int leaf(int rank, int chunk, int nChunks) {
+    const int key = rank * nChunks + chunk;
+    auto it = leaves_.find(key);
+    if (it != leaves_.end()) return it->second;
+    nodes_.push_back({-1, key});
+    return leaves_[key] = (int)nodes_.size() - 1;
+  }
+  int op(int x, int y) {
+    if (x < 0 || y < 0) return kUndef;  // an uninitialised chunk poisons the result
+    const std::pair<int, int> k = x < y ? std::make_pair(x, y) : std::make_pair(y, x);
+    auto it = ops_.find(k);
+    if (it != ops_.end()) return it->second;
+    nodes_.push_back({k.first, k.second});
+    return ops_[k] = (int)nodes_.size() - 1;
+  }
+  const Expr& at(int i) const { return nodes_[i]; }
+  static constexpr int kUndef = -1;
+
+ private:
+  std::vector<Expr> nodes_;
+  std::map<int, int> leaves_;
+  std::map<std::pair<int, int>, int> ops_;
+};
+
+struct TbState {
+  size_t pc = 0;      // next transfer
+  int step = 0;       // the interpreter's XML step counter
+  int published = -1;
+};
+
+}  // namespace
+
+FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
+  FoldLowering out;
+  const int n = (int)byRank.size();
+  auto fail = [&](const std::string& why) {
+    out.ok = false;
+    out.why = why;
+    out.order.clear();
+    return out;
+  };
+  if (n < 2 || n > kMaxReduceFusion) return fail("ranks outside 2..16");
+  const Algorithm& a0 = byRank[0];
+  const int C = a0.nchunksPerLoop;
+  if (C <= 0) return fail("no chunks");
+  for (const Algorithm& a : byRank) {
+    if (!a.valid || a.coll != kAllReduce) return fail("not a valid AllReduce schedule");
+    if (a.proto != kProtoLL) return fail("protocol is not LL");
+    if (a.nchunksPerLoop != C || a.inPlace != a0.inPlace) return fail("ranks disagree on the loop shape");
+  }
+  Exprs ex;
+  // buffers per rank: input, output (aliases the input in place), scratch
+  std::vector<std::vector<int>> inB(n), outB(n), scrB(n);
+  for (int r = 0; r < n; r++) {
+    const Algorithm& a = byRank[r];
+    inB[r].assign(std::max(C, a.nInputChunks), Exprs::kUndef);
+    for (int c = 0; c < (int)inB[r].size(); c++) inB[r][c] = c < C ? ex.leaf(r, c, C) : Exprs::kUndef;
+    if (!a.inPlace) outB[r].assign(std::max(C, a.nOutputChunks), Exprs::kUndef);
+    scrB[r].assign(std::max(0, a.nScratchChunks), Exprs::kUndef);
+  }
+  auto buf = [&](int r, int id) -> std::vector<int>* {
+    if (id == kInput) return &inB[r];
+    if (id == kOutput) return byRank[r].inPlace ? &inB[r] : &outB[r];
+    if (id == kScratch) return &scrB[r];
+    return nullptr;
+  };
+  // FIFO of messages per (channel, sender, receiver)
+  std::map<std::tuple<int, int, int>, std::vector<std::vector<int>>> fifo;
+  std::vector<std::vector<TbState>> st(n);
+  for (int r = 0; r < n; r++) st[r].assign(byRank[r].nBlocks, TbState());
+  bool progress = true;
+  size_t guard = 0;
+  while (progress) {
+    progress = false;
+    for (int r = 0; r < n; r++) {
+      const Algorithm& a = byRank[r];
+      for (int b = 0; b < a.nBlocks; b++) {
+        const ThreadBlock& tb = a.tbs[b];
+        TbState& s = st[r][b];
+        while (s.pc < tb.transfers.size()) {
+          if (++guard > (size_t)1 << 24) return fail("schedule too large to analyse");
+          const Transfer& t = tb.transfers[s.pc];
+          bool ready = true;
+          for (int d = 0; d < t.numDeps && ready; d++) {
+            const int db = tb.depBid[t.depPtr + d], ds = tb.depStep[t.depPtr + d];
+            if (db < 0 || db >= a.nBlocks) return fail("dependency on a missing thread block");
+            ready = st[r][db].published >= ds;
+          }
+          const bool recv = t.type == kRecv || t.type == kRecvCopySend || t.type == kRecvReduceSend ||
+                            t.type == kRecvReduceCopy || t.type == kRecvReduceCopySend;
+          const bool send = t.type == kSend || t.type == kRecvCopySend || t.type == kRecvReduceSend ||
+                            t.type == kRecvReduceCopySend;
+          std::vector<std::vector<int>>* in = nullptr;
+          if (ready && recv) {
+            if (tb.recvpeer < 0) return fail("receive without a peer");
+            in = &fifo[std::make_tuple((int)tb.channel, (int)tb.recvpeer, r)];
+            ready = !in->empty();
+          }
+          if (!ready) break;
+          if (send && tb.sendpeer < 0) return fail("send without a peer");
+          const int cnt = t.count;
+          std::vector<int>* src = buf(r, t.srcbuf);
+          std::vector<int>* dst = buf(r, t.dstbuf);
+          auto rd = [&](std::vector<int>* v, int off) -> int {
+            if (v == nullptr || off < 0 || off >= (int)v->size()) return Exprs::kUndef;
+            return (*v)[off];
+          };
+          auto wr = [&](std::vector<int>* v, int off, int x) -> bool {
+            if (v == nullptr || off < 0 || off >= (int)v->size()) return false;
+            (*v)[off] = x;
+            return true;
+          };
+          std::vector<int> msg;
+          if (recv) {
+            msg = in->front();
+            in->erase(in->begin());
+            if ((int)msg.size() != cnt) return fail("receive count differs from the matching send");
+          }
+          std::vector<int> outMsg;
+          switch (t.type) {
+            case kSend:
+              for (int c = 0; c < cnt; c++) outMsg.push_back(rd(src, t.srcoff + c));
+              break;
+            case kRecv:
+              for (int c = 0; c < cnt; c++)
+                if (!wr(dst, t.dstoff + c, msg[c])) return fail("receive into a missing chunk");
+              break;
+            case kRecvCopySend:
+              for (int c = 0; c < cnt; c++)
+                if (!wr(dst, t.dstoff + c, msg[c])) return fail("receive into a missing chunk");
+              outMsg = msg;
+              break;
+            case kRecvReduceSend:
+            case kRecvReduceCopy:
+            case kRecvReduceCopySend:
+              for (int c = 0; c < cnt; c++) {
+                const int v = ex.op(msg[c], rd(src, t.srcoff + c));  // fn(peer, local)
+                if (t.type != kRecvReduceSend && !wr(dst, t.dstoff + c, v)) return fail("write to a missing chunk");
+                if (t.type != kRecvReduceCopy) outMsg.push_back(v);
+              }
+              break;
+            case kLocalCopy: {
+              std::vector<int> v;
+              for (int c = 0; c < cnt; c++) v.push_back(rd(src, t.srcoff + c));
+              for (int c = 0; c < cnt; c++)
+                if (!wr(dst, t.dstoff + c, v[c])) return fail("copy to a missing chunk");
+              break;
+            }
+            case kReduce:
+              for (int c = 0; c < cnt; c++) {
+                int acc = rd(dst, t.dstoff + c);
+                for (int j = 0; j < t.numReds; j++) acc = ex.op(acc, rd(src, tb.redSrcOff[t.redPtr + j] + c));
+                if (!wr(dst, t.dstoff + c, acc)) return fail("reduce into a missing chunk");
+              }
+              break;
+            default:
+              return fail("transfer type without a lowering (res-add or unknown)");
+          }
+          if (send) fifo[std::make_tuple((int)tb.channel, r, (int)tb.sendpeer)].push_back(outMsg);
+          if (t.numDeps > 0) s.step += t.numDeps - 1;
+          if (t.type == kReduce) s.step += t.numReds - 1;
+          if (t.hasDep) s.published = s.step;
+          s.step++;
+          s.pc++;
+          progress = true;
+        }
+      }
+    }
+  }
+  for (int r = 0; r < n; r++)
+    for (int b = 0; b < byRank[r].nBlocks; b++)
+      if (st[r][b].pc < byRank[r].tbs[b].transfers.size()) return fail("schedule does not complete");
+  for (auto& kv : fifo)
+    if (!kv.second.empty()) return fail("unconsumed FIFO messages");
+  // every result chunk: a left fold of all ranks' same chunk, one order per rank
+  out.order.assign(n, {});
+  for (int r = 0; r < n; r++) {
+    const std::vector<int>& res = byRank[r].inPlace ? inB[r] : outB[r];
+    if (!byRank[r].inPlace)
+      for (int c = 0; c < C; c++)
+        if (inB[r][c] != ex.leaf(r, c, C)) return fail("an out-of-place schedule writes its input");
+    for (int c = 0; c < C; c++) {
+      std::vector<int> ord;  // ranks, outermost fold last
+      int e = res[c];
+      if (e < 0) return fail("a result chunk is not a fold of the inputs");
+      while (ex.at(e).a >= 0) {
+        const Expr& x = ex.at(e);
+        const bool la = ex.at(x.a).a < 0, lb = ex.at(x.b).a < 0;
+        if (la && lb) {
+          // the innermost fn(x_p, x_q): commutative, so the fold may start with either
+          int p = ex.at(x.a).b, q = ex.at(x.b).b;
+          if (p > q) std::swap(p, q);
+          ord.push_back(q);
+          ord.push_back(p);
+          e = -1;
+          break;
+        }
+        if (!la && !lb) return fail("a result chunk folds partial results in a tree shape");
+        ord.push_back(la ? ex.at(x.a).b : ex.at(x.b).b);
+        e = la ? x.b : x.a;
+      }
+      if (e >= 0) ord.push_back(ex.at(e).b);  // a lone leaf (no fold)
+      std::vector<int> ranks;
+      std::vector<bool> seen(n, false);
+      for (auto it = ord.rbegin(); it != ord.rend(); ++it) {
+        const int q = *it / C, cc = *it % C;
+        if (cc != c || seen[q]) return fail("a result chunk is not a fold of every rank's same chunk");
+        seen[q] = true;
+        ranks.push_back(q);
+      }
+      if ((int)ranks.size() != n) return fail("a result chunk misses a rank");
+      if (c == 0) out.order[r] = ranks;
+      else if (ranks != out.order[r]) return fail("the fold order differs between chunks of one rank");
+    }
+  }
+  out.ok = true;
+  return out;
+}
+
+}  // namespace msccl

@@ -81,6 +81,8 @@ Knobs Knobs::fromEnv() {
   k.smallKernel = envInt("MSCCL_AMD_SMALL_KERNEL", 1) != 0;
   k.fuse = envInt("MSCCL_AMD_FUSE", 1) != 0;
   k.treeFlat = envInt("MSCCL_AMD_TREE_FLAT", 1) != 0;
+  k.lower = envInt("MSCCL_AMD_LOWER", 1) != 0;
+  k.lowerMaxBytes = envInt("MSCCL_AMD_LOWER_MAX_BYTES", 32 << 10);
   return k;
 }
 
@@ -274,6 +276,27 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   p->maxAllowedCount = (int)std::min<int64_t>(kMaxCount - 1, std::max<int64_t>(1, (stepSize / 2) / std::max<int64_t>(1, p->nBytes)));
   p->chunkSize = (int64_t)(int)(stepSize / 2 / ts);
   p->minChunk = std::max<int64_t>(1, (int64_t)nt * (8 / ts));
+  p->sizePerChunk = p->count;
+  p->nIters = (int)((p->sizePerChunk + p->chunkSize - 1) / p->chunkSize);
+  p->scratchNeeded = 0;
+  return 0;
+}
+
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, Plan* p) {
+  if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > k.lowerMaxBytes ||
+      p->nBytes > (1ll << 30))
+    return 1;
+  // the fold kernel's chunk math (makeFlatTreePlan): one call over the whole buffer
+  const int ts = refTypeSize(p->dtype);
+  const int64_t stepSize = k.buffSizes[kProtoLL] / kFifoSteps;
+  p->ringColl = kTreeFlat;
+  p->flatColl = kRingAllReduce;
+  p->ringChannels = 0;
+  p->nchunksPerLoop = 1;
+  p->sizeMultiplier = 1;
+  p->maxAllowedCount = (int)std::min<int64_t>(kMaxCount - 1, std::max<int64_t>(1, (stepSize / 2) / std::max<int64_t>(1, p->nBytes)));
+  p->chunkSize = (int64_t)(int)(stepSize / 2 / ts);
+  p->minChunk = std::max<int64_t>(1, (int64_t)p->refNthreads * (8 / ts));
   p->sizePerChunk = p->count;
   p->nIters = (int)((p->sizePerChunk + p->chunkSize - 1) / p->chunkSize);
   p->scratchNeeded = 0;

@@ -75,6 +75,9 @@ struct Knobs {
   int32_t referenceSelection;  // MSCCL_AMD_REFERENCE_SELECTION: the reference's MSCCL gating (below)
   int32_t fuse;              // MSCCL_AMD_FUSE: fused s + rrc exchanges (transport.cc: fusableTbs)
   int32_t treeFlat;          // MSCCL_AMD_TREE_FLAT: the tree's values in one hop (plan.cc: makeFlatTreePlan)
+  int32_t lower;             // MSCCL_AMD_LOWER: one-hop AllReduce schedules run as the fold (lower.cc)
+  int32_t pad0;
+  int64_t lowerMaxBytes;     // MSCCL_AMD_LOWER_MAX_BYTES: largest call (bytes per rank) lowered
   static Knobs fromEnv();
 };
 
@@ -108,5 +111,10 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p);
 //   its block to every peer and stores each peer's at its place (AllGather), instead of n - 1.
 // Returns 0, or nonzero when the call does not qualify (the plan is then unchanged).
 int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p);
+// A call of an MSCCL AllReduce schedule that lower.cc proved to be a one-hop fold (LL, op
+// Sum..Min, at most MSCCL_AMD_LOWER_MAX_BYTES per rank): turns the schedule's plan into the fold
+// kernel's (ringColl kTreeFlat, flatColl kRingAllReduce; algoIndex kept: the fold runs with the
+// schedule's own fold order, ncclComm::foldAlgos).  Returns 0, or nonzero (plan unchanged).
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, Plan* p);
 
 }  // namespace msccl

@@ -467,8 +467,11 @@ ncclResult_t ringUpload(ncclComm* comm) {
         if (rp[b] == q) return b;
       return -1;
     };
+    // arOrder: the AllReduce's fold order (ranks); the flat tree's is n-1 .. 0, a lowered
+    // schedule's its own (lower.cc)
+    auto foldImage = [&](const std::vector<int>& arOrder, DevAlgoHost& d) -> ncclResult_t {
     std::vector<int16_t> reds;
-    for (int q = n - 1; q >= 0; q--) reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
+    for (int q : arOrder) reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
     for (int i = 1; i <= n; i++) {
       const int q = (r + i) % n;
       reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
@@ -484,7 +487,6 @@ ncclResult_t ringUpload(ncclComm* comm) {
       ts[i].numReds = (int16_t)n;
       ts[i].redPtr = (int16_t)(i * n);
     }
-    DevAlgoHost& d = comm->ringAlgos[5];
     d.nBlocks = 1;
     d.tbStride = (int)imageBytes(ts.size(), 0, reds.size());
     d.connSplit = kFlatSubs;
@@ -497,7 +499,16 @@ ncclResult_t ringUpload(ncclComm* comm) {
     h.nreds = (uint16_t)reds.size();
     const std::vector<int16_t> none;
     putImage(img, 0, h, ts, none, none, reds);
-    NCCLCHECK(uploadImages(img, &d));
+    return uploadImages(img, &d);
+    };
+    std::vector<int> chain;
+    for (int q = n - 1; q >= 0; q--) chain.push_back(q);
+    NCCLCHECK(foldImage(chain, comm->ringAlgos[5]));
+    // the one-hop MSCCL schedules (lower.cc): the fold with the schedule's order, over the same
+    // flat connections (the step counters are the connections', whichever program runs)
+    comm->foldAlgos.assign(comm->algos.size(), DevAlgoHost());
+    for (size_t g = 0; g < comm->algoFoldOrder.size(); g++)
+      if (!comm->algoFoldOrder[g].empty()) NCCLCHECK(foldImage(comm->algoFoldOrder[g], comm->foldAlgos[g]));
   }
   return ncclSuccess;
 }

@@ -1,0 +1,108 @@
+"""One-hop MSCCL AllReduce schedules lowered to the fold kernel on the GPU (msccl_amd/csrc/lower.cc).
+
+A call of a schedule that lower.cc proves to be a one-hop fold (LL, op Sum..Min, at most
+MSCCL_AMD_LOWER_MAX_BYTES per rank) runs mscclFoldKernel with the schedule's fold order.  Every
+result here is compared bit for bit with oracle/sim.py running the XML itself (the reference's
+interpreter semantics), and the comm info names the kernel that ran: last.small == 2 (the fold)
+with last.algo the schedule's index, or 1 / 0 (the interpreter)."""
+import os
+
+import numpy as np
+import pytest
+
+from msccl_amd import xmlgen
+from oracle import loader as L
+from oracle import numerics as N
+from tests.gpu_harness import CoResident, describe_mismatch, from_torch, gen_inputs, to_torch
+
+pytestmark = pytest.mark.gpu
+os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
+
+
+def _bench():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import bench
+    return bench
+
+
+def _case(cr, count, dt, seed, op=0, in_place=True):
+    import torch
+    dev = torch.device("cuda:0")
+    ins = gen_inputs(cr.n, count, dt, seed)
+    t = [to_torch(x, dev) for x in ins]
+    outs = t if in_place else [torch.zeros_like(x) for x in t]
+    torch.cuda.synchronize()
+    cr.run(L.ALLREDUCE, count, dt, op, [x.data_ptr() for x in t], [x.data_ptr() for x in outs])
+    gpu = [from_torch(x, N.storage(dt)) for x in outs]
+    want, used = cr.oracle(L.ALLREDUCE, count, dt, op, ins, in_place)
+    for r in range(cr.n):
+        assert np.array_equal(gpu[r].view(np.uint8), want[r].view(np.uint8)), \
+            "rank %d count %d dt %d op %d (schedule %s)\n%s" % (r, count, dt, op, used, describe_mismatch(gpu[r], want[r]))
+    return cr.comms[0].info()["last"], used
+
+
+@pytest.mark.parametrize("nbytes", [128, 1024, 4096, 16384, 32768])
+def test_c2_pair_tiers_lowered(tmp_path, nbytes):
+    """C2 (2 ranks, fp32) through bench.py's tiers: calls up to 32 KiB run the fold kernel."""
+    tiers = _bench().make_xmls(2, "LL", 16, str(tmp_path))
+    with CoResident(2, [open(t[3]).read() for t in tiers], str(tmp_path)) as cr:
+        for rep in range(3):
+            last, used = _case(cr, nbytes // 4, 7, 10 * rep + nbytes % 89)
+            assert last["small"] == 2 and last["algo"] == used and last["ringColl"] == 5, last
+
+
+@pytest.mark.parametrize("nbytes", [128, 2048, 8192])
+@pytest.mark.parametrize("dt", [6, 9])
+def test_c3_oneshot_tier_lowered(tmp_path, nbytes, dt):
+    """C3's small tier (8 ranks, rank-ordered one-shot x4, fp16 / bf16): the fold in rank order."""
+    tiers = _bench().make_xmls(8, "LL", 4, str(tmp_path))
+    with CoResident(8, [open(t[3]).read() for t in tiers], str(tmp_path)) as cr:
+        last, used = _case(cr, nbytes // 2, dt, nbytes % 97)
+        assert last["small"] == 2 and last["algo"] == used == 0, last
+
+
+@pytest.mark.parametrize("op", [0, 1, 2, 3])
+def test_unordered_oneshot_every_op(tmp_path, op):
+    """The unordered one-shot: every rank folds its own input first (a different order per rank,
+    different fp16 bits per rank), out of place too."""
+    xml = xmlgen.allreduce_oneshot(4, 2, "LL")
+    with CoResident(4, [xml], str(tmp_path)) as cr:
+        last, _ = _case(cr, 2 * 1000, 6, 20 + op, op=op)
+        assert last["small"] == 2, last
+    xml = xmlgen.allreduce_pair_oneshot(2, "LL", inplace=False)
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        last, _ = _case(cr, 2 * 777, 9, 30 + op, op=op, in_place=False)
+        assert last["small"] == 2, last
+
+
+def test_knobs_and_limit(tmp_path, monkeypatch):
+    """MSCCL_AMD_LOWER=0 keeps the interpreter; calls above MSCCL_AMD_LOWER_MAX_BYTES keep it too."""
+    xml = xmlgen.allreduce_pair_oneshot(4, "LL")
+    monkeypatch.setenv("MSCCL_AMD_LOWER", "0")
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        last, _ = _case(cr, 1024, 7, 1)
+        assert last["small"] == 1, last
+    monkeypatch.setenv("MSCCL_AMD_LOWER", "1")
+    monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "4096")
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        assert _case(cr, 1024, 7, 2)[0]["small"] == 2
+        assert _case(cr, 1028, 7, 3)[0]["small"] == 1
+
+
+def test_lowered_interpreted_and_flat_calls_interleave(tmp_path, monkeypatch):
+    """The lowered schedule shares the flat connections with the fallback's flat tree, and its
+    own connections stay with its interpreted calls: 200 launches mixing the three, across the
+    8-bit LL flag wrap and cleanup (MSCCL_AMD_TEST_LL_CLEANUP=1), every result bit-exact."""
+    monkeypatch.setenv("MSCCL_AMD_TEST_LL_CLEANUP", "1")
+    xml = xmlgen.allreduce_oneshot(4, 2, "LL", ordered=True, max_bytes=1 << 20)
+    with CoResident(4, [xml], str(tmp_path)) as cr:
+        kinds = set()
+        for it in range(200):
+            k = it % 3
+            count = (2048, 2 * 40000, 2 * 3001 + 1)[k]   # lowered, interpreted, no schedule (flat tree)
+            last, used = _case(cr, count, 6, it)
+            kinds.add((k, last["small"], used))
+        assert kinds == {(0, 2, 0), (1, 1, 0), (2, 2, "ring")}, kinds

@@ -315,3 +315,34 @@ def test_remote_ordering_path(proto, monkeypatch):
     monkeypatch.setenv("MSCCL_AMD_FORCE_REMOTE", "1")
     check(xmlgen.allreduce_allpairs(4, 2, proto), 4, L.ALLREDUCE, 32 * 5001, 7)
     check(xmlgen.allreduce_ring(4, 2, proto), 4, L.ALLREDUCE, 8 * 7777, 9)
+
+
+def test_schedules_interleaved_with_multi_workgroup_fold_calls(tmp_path, monkeypatch):
+    """Every schedule owns its flag / epoch slots (init.cc: allocSlots).  Fallback calls that run
+    the fold kernel with four workgroups (count >= 4 x 512 packs) alternate with a loaded split-1
+    all-pairs schedule whose thread blocks wait on each other's flags: a fold launch must never
+    advance an epoch another schedule's workgroup has yet to read (before the per-schedule ranges,
+    a fold workgroup's epilogue wrote slots 1..3, which other fold workgroups read at their start
+    when maxSplit was 1).  Every result bit-exact against the oracle, no wait times out."""
+    import torch
+    from tests.gpu_harness import CoResident, gen_inputs, to_torch, from_torch
+    from oracle import numerics as N
+    monkeypatch.setenv("MSCCL_AMD_SPLIT", "1")
+    monkeypatch.setenv("MSCCL_AMD_TIMEOUT_SEC", "20")
+    n = 2
+    xml = xmlgen.allreduce_allpairs(n, 1, "LL", max_bytes=4096)
+    dev = torch.device("cuda:0")
+    with CoResident(n, [xml], str(tmp_path)) as cr:
+        assert cr.comms[0].info()["maxSplit"] == 1
+        for it in range(6):
+            for count, want_fold in ((4 * 512 * 4, True), (512, False)):
+                ins = gen_inputs(n, count, 7, 100 * it + count % 97)
+                t = [to_torch(x, dev) for x in ins]
+                torch.cuda.synchronize()
+                cr.run(L.ALLREDUCE, count, 7, 0, [x.data_ptr() for x in t], [x.data_ptr() for x in t])
+                last = cr.comms[0].info()["last"]
+                assert (last["small"] == 2 and last["split"] == 4) if want_fold else last["algo"] == 0, last
+                want, _ = cr.oracle(L.ALLREDUCE, count, 7, 0, ins, True)
+                for r in range(n):
+                    got = from_torch(t[r], N.storage(7))
+                    assert np.array_equal(got.view(np.uint32), want[r].view(np.uint32)), (it, count, r)
