@@ -74,6 +74,7 @@ struct ncclComm {
   // per algorithm: this rank's fold order when the schedule runs as the one-hop fold (lower.cc;
   // empty: it does not) and the fold kernel's program for it (nBlocks 0 when empty)
   std::vector<std::vector<int>> algoFoldOrder;
+  std::vector<int> algoSet;  // per algorithm: the small kernel's transfer set (transport.cc: algoUpload)
   std::vector<msccl::DevAlgoHost> foldAlgos;
   msccl::DevAlgoHost ringAlgos[6];  // ring fallback programs, [4] = tree, [5] = flat tree (transport.cc: ringUpload)
   msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank
@@ -135,6 +136,7 @@ struct ncclComm {
   // what the most recent collective ran (introspection: mscclAmdCommInfo "last")
   struct LastLaunch {
     int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0, small = 0;
+    int set = 0;  // the small kernel's transfer set (devcomm.h: kSetAll / kSetExchange)
   } last;
 
   // user reduction ops (ncclRedOpCreatePreMulSum, enqueue.cc:1529-1580): a free list as in the

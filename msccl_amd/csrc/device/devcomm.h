@@ -227,6 +227,14 @@ using LaunchArgs = LaunchArgsN<kMaxLaunchRanks>;
 // copies the whole block per launch, about 0.9 us more for the larger one (tools/host_lat).
 constexpr int kCompactLaunchRanks = 2;
 
+// Transfer-type sets of the small-call kernel (mscclSmallKernel<..., SET>).  A launch's code is
+// fetched into the instruction cache anew by every workgroup's CU, and the general kernel inlines
+// every primitive (135 KB for fp32 Sum): the pair exchange ran 1.0-1.1 us faster per launch in a
+// kernel holding only its own transfers (2 ranks, 128 B - 64 KiB, graph replay, same box:
+// profiles/r04a_lat.txt).  kSetExchange: programs of `s`, `rrc` and the fused s + rrc only (the
+// 2-rank pair exchange, xmlgen.allreduce_pair_oneshot; enqueue.cc picks it per launch).
+enum : int { kSetAll = 0, kSetExchange = 1 };
+
 // Error codes in DevComm::errWord
 enum : uint32_t { kDevOk = 0, kDevTimeout = 1, kDevAbort = 2, kDevBadOp = 3 };
 
@@ -236,7 +244,7 @@ typedef int (*OneRankFn)(const void* src, void* dst, size_t n, uint64_t arg, int
 OneRankFn getOneRankFn(int dtype);
 constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = resident workgroups per CU
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
-LaunchFn getSmallLaunchFn(int dtype, int redop);  // mscclSmallKernel (LL, Sum..Min), or null
+LaunchFn getSmallLaunchFn(int dtype, int redop, int set);  // mscclSmallKernel (LL, Sum..Min, kSet*), or null
 LaunchFn getFoldLaunchFn(int dtype, int redop);   // mscclFoldKernel (the flat tree), or null
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):
 // NPKit's host/GPU clock calibration.  Returns 0 on a successful launch.

@@ -2,7 +2,7 @@
 #include "devcomm.h"
 
 namespace msccl {
-#define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[4]; extern LaunchFn N##_fold[4]; extern OneRankFn N##_one;
+#define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[2][4]; extern LaunchFn N##_fold[4]; extern OneRankFn N##_one;
 MSCCL_DECL(gLaunch_i8)
 MSCCL_DECL(gLaunch_u8)
 MSCCL_DECL(gLaunch_i32)
@@ -23,12 +23,13 @@ LaunchFn getLaunchFn(int dtype, int devOp, int proto) {
   return tabs[dtype][devOp][proto];
 }
 
-// the small-call kernel (mscclSmallKernel): LL, devOp Sum..Min
-LaunchFn getSmallLaunchFn(int dtype, int devOp) {
-  LaunchFn* tabs[10] = {gLaunch_i8_small, gLaunch_u8_small, gLaunch_i32_small, gLaunch_u32_small, gLaunch_i64_small,
-                        gLaunch_u64_small, gLaunch_f16_small, gLaunch_f32_small, gLaunch_f64_small, gLaunch_bf16_small};
-  if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
-  return tabs[dtype][devOp];
+// the small-call kernel (mscclSmallKernel): LL, devOp Sum..Min, transfer set kSetAll / kSetExchange
+LaunchFn getSmallLaunchFn(int dtype, int devOp, int set) {
+  LaunchFn(*tabs[10])[4] = {gLaunch_i8_small, gLaunch_u8_small, gLaunch_i32_small, gLaunch_u32_small,
+                            gLaunch_i64_small, gLaunch_u64_small, gLaunch_f16_small, gLaunch_f32_small,
+                            gLaunch_f64_small, gLaunch_bf16_small};
+  if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3 || set < 0 || set > 1) return nullptr;
+  return tabs[dtype][set][devOp];
 }
 
 // the flat tree's fold kernel (mscclFoldKernel): LL, devOp Sum..Min

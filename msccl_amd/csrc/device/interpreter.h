@@ -1045,23 +1045,21 @@ struct Interp {
 
   // One primitive call of transfer t; false for MSCCL_RES_ADD / unknown types (the tb ends,
   // msccl_interpreter.h:195-196).  `reOff` is the chunk offset of a fused reduction's sources.
-  template <bool FUSE>
+  template <bool FUSE, int SET = kSetAll>
   __device__ __forceinline__ bool exec(const DevTransfer& t, T* srcP, T* dstP, int64_t srcoff, int64_t dstoff,
                                        int64_t reOff, int64_t sizePer, const Shape& s) {
-#ifdef MSCCL_EXP_COMPACT
-    // measurement build: the small kernel with the pair exchange's transfers only (code size A/B)
-    if constexpr (FUSE) {
+    if constexpr (SET == kSetExchange) {
+      // the exchange kernels (devcomm.h: kSetExchange): the pair exchange's transfers only
       switch (t.type) {
         case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
         case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
         case tSendRrc:
-          if constexpr (PROTO == pLL && OP <= 3) [[clang::always_inline]] llFusedOp(srcP + srcoff, dstP + dstoff, s);
+          if constexpr (FUSE && PROTO == pLL && OP <= 3) [[clang::always_inline]] llFusedOp(srcP + srcoff, dstP + dstoff, s);
           break;
         default: return false;
       }
       return true;
     }
-#endif
     switch (t.type) {
       case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
       case tRecv: op<1, 0, 0, 1>(nullptr, dstP + dstoff, s); break;
@@ -1361,8 +1359,23 @@ struct Interp {
     scG = nullptr;
     rcG = nullptr;
     const int np = w.foldPeers;
+    constexpr int E = 8 / TS;
+    constexpr int G = 8;  // peers per wait
+    const int n = (int)w.sizePerChunk;
+    const int npkAll = (n + PE - 1) / PE;
+    // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges,
+    // cut into FIFO steps on its own sub-connection of every peer
+    const int p0 = (int)((int64_t)npkAll * wg / w.split);
+    const int npk = (int)((int64_t)npkAll * (wg + 1) / w.split) - p0;
+    const int nlinesFull = (n + E - 1) / E;
+    const __amdgpu_buffer_rsrc_t srs = makeRsrc(w.sendbuff), drs = makeRsrc(w.recvbuff);
+    const bool vec = aligned16(w.sendbuff) && aligned16(w.recvbuff);
     // one round trip: thread block 0's image (the fold order), every peer's send and recv
-    // records, the launch epoch
+    // records, the launch epoch, and this lane's first input pack (step 0, q = tid: the pack
+    // p0 + tid in every FIFO cut; the ReduceScatter reads the blocks the image names instead),
+    // so the input's load does not wait for the image's
+    u32x4 pre = {0, 0, 0, 0};
+    const bool havePre = w.ringColl != kRingReduceScatter && tid < npk;
     {
       const u32x4* gimg = (const u32x4*)w.images;
       const int nU = w.tbStride >> 4;
@@ -1379,6 +1392,7 @@ struct Interp {
         sh->aborted = 0;
         sh->epoch = atomicLoadAgent(w.epochs + wg);  // slot wg of the fold's range
       }
+      if (havePre) pre = loadPack(srs, vec, p0 + tid, n);
     }
     __syncthreads();
     const uint64_t workIndex = uni(sh->epoch);
@@ -1407,17 +1421,6 @@ struct Interp {
         nq++;
       }
     }
-    constexpr int E = 8 / TS;
-    constexpr int G = 8;  // peers per wait
-    const int n = (int)w.sizePerChunk;
-    const int npkAll = (n + PE - 1) / PE;
-    // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges,
-    // cut into FIFO steps on its own sub-connection of every peer
-    const int p0 = (int)((int64_t)npkAll * wg / w.split);
-    const int npk = (int)((int64_t)npkAll * (wg + 1) / w.split) - p0;
-    const int nlinesFull = (n + E - 1) / E;
-    const __amdgpu_buffer_rsrc_t srs = makeRsrc(w.sendbuff), drs = makeRsrc(w.recvbuff);
-    const bool vec = aligned16(w.sendbuff) && aligned16(w.recvbuff);
     const int slotLines = uni(fs->foldRecv[0].llSlotLines);
     const int slotPacks = slotLines / 2;
     ev(kEvSetup, 0, 0);
@@ -1468,7 +1471,7 @@ struct Interp {
           }
           own = loadBlockPack((const T*)w.sendbuff, uni((int)rankOf[np]), n, B);
         } else {
-          own = loadPack(srs, vec, B, n);
+          own = s0 == 0 && q == tid && havePre ? pre : loadPack(srs, vec, B, n);
           for (int k = 0; k < np; k++) {  // the send: this pack to every peer
             const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[k].out);
             const uint32_t f = fs->fold[k].sflag;
@@ -1600,6 +1603,7 @@ struct Interp {
   // each end of a connection may run either kernel), the flags (iter = pass) and the primitives
   // are run()'s; what goes is the 64-bit iteration arithmetic and most of the scalar state the
   // big loop keeps live (SGPR spills), a few us per launch.
+  template <int SET>
   __device__ __forceinline__ void runSmall(const RankWork& w, int local) {
     const uint64_t tStart = w.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // MSCCL_AMD_TRACE=2
     redArg = 0;
@@ -1663,7 +1667,7 @@ struct Interp {
             s.Lq = q1 - q0;
             s.npk = thisCount * s.Lq;
           }
-          if (!exec<true>(t, srcP, dstP, grid + (t.srcoff + c) * sizePer, grid + (td.dstoff + c) * sizePer,
+          if (!exec<true, SET>(t, srcP, dstP, grid + (t.srcoff + c) * sizePer, grid + (td.dstoff + c) * sizePer,
                     grid + c * sizePer, sizePer, s))
             return false;
           if (t.type == tRe && c == 0) step += t.numReds - 1;
@@ -1678,12 +1682,10 @@ struct Interp {
       }
       return true;
     };
-#ifdef MSCCL_EXP_COMPACT
-    if (false) {
-#else
-    if (whole) {
-#endif
-      runPass(0, 0);  // the common small call: no pass loop state
+    // the common small call: one pass without loop state; the exchange kernels keep only the loop
+    // (one instance of runPass: less code to fetch per launch)
+    if (SET != kSetExchange && whole) {
+      runPass(0, 0);
     } else {
       for (int grid = 0, iter = 0; grid < sizePer; grid += nelem, iter++)
         if (!runPass(grid, iter)) break;
@@ -1737,8 +1739,8 @@ __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
 }
 
 // Small-call variant (Interp::runSmall): every RankWork of the launch is one interpreter
-// iteration of an MSCCL schedule.
-template <typename T, int OP, int PROTO, int R>
+// iteration of an MSCCL schedule.  SET: the transfer types its programs use (devcomm.h).
+template <typename T, int OP, int PROTO, int R, int SET>
 __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> args) {
   __shared__ BlockShared sh;
   int b = blockIdx.x;
@@ -1747,7 +1749,7 @@ __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> 
   const RankWork& w = args.w[r];
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
-  it.runSmall(w, b - w.blockBase);
+  it.template runSmall<SET>(w, b - w.blockBase);
 }
 
 // The flat tree's fold kernel (Interp::runFold): rank r of the launch owns workgroups

@@ -21,14 +21,14 @@ int launchKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
 
 // the small-call kernel (mscclSmallKernel, LL): same contract as launchKernel; launches of at
 // most kCompactLaunchRanks ranks take the variant with the compact argument block
-template <typename T, int OP, int PROTO>
+template <typename T, int OP, int PROTO, int SET>
 int launchSmallKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   constexpr int RC = kCompactLaunchRanks;
   if (gridBlocks == kQueryResidency) {
     int n = 0, m = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclSmallKernel<T, OP, PROTO, kMaxLaunchRanks>, kNT, 0) !=
-            hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, mscclSmallKernel<T, OP, PROTO, RC>, kNT, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclSmallKernel<T, OP, PROTO, kMaxLaunchRanks, SET>, kNT,
+                                                     0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, mscclSmallKernel<T, OP, PROTO, RC, SET>, kNT, 0) != hipSuccess)
       return 0;
     return n < m ? n : m;
   }
@@ -37,9 +37,9 @@ int launchSmallKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
     a.nRanks = args.nRanks;
     a.pad = 0;
     for (int r = 0; r < RC; r++) a.w[r] = args.w[r];
-    hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO, RC>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO, RC, SET>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
   } else {
-    hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO, kMaxLaunchRanks>), dim3(gridBlocks), dim3(kNT), 0,
+    hipLaunchKernelGGL((mscclSmallKernel<T, OP, PROTO, kMaxLaunchRanks, SET>), dim3(gridBlocks), dim3(kNT), 0,
                        (hipStream_t)stream, args);
   }
   return hipGetLastError() == hipSuccess ? 0 : 1;
@@ -101,8 +101,11 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
       {launchKernel<T, kPreMulSum, pLL>, nullptr, launchKernel<T, kPreMulSum, pSimple>}
 // Small-call kernels: MSCCL schedules (ops Sum..Min) on LL.
 #define MSCCL_SMALL(NAME, T)                                                                               \
-  LaunchFn NAME##_small[4] = {launchSmallKernel<T, kSum, pLL>, launchSmallKernel<T, kProd, pLL>,          \
-                              launchSmallKernel<T, kMax, pLL>, launchSmallKernel<T, kMin, pLL>};          \
+  LaunchFn NAME##_small[2][4] = {                                                                          \
+      {launchSmallKernel<T, kSum, pLL, kSetAll>, launchSmallKernel<T, kProd, pLL, kSetAll>,                 \
+       launchSmallKernel<T, kMax, pLL, kSetAll>, launchSmallKernel<T, kMin, pLL, kSetAll>},                 \
+      {launchSmallKernel<T, kSum, pLL, kSetExchange>, launchSmallKernel<T, kProd, pLL, kSetExchange>,       \
+       launchSmallKernel<T, kMax, pLL, kSetExchange>, launchSmallKernel<T, kMin, pLL, kSetExchange>}};      \
   LaunchFn NAME##_fold[4] = {launchFoldKernel<T, kSum>, launchFoldKernel<T, kProd>, launchFoldKernel<T, kMax>, \
                              launchFoldKernel<T, kMin>};
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \

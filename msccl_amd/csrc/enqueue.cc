@@ -381,10 +381,21 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   const Planned& p0 = *ps[0];
   // a launch group holds flat-tree works only or none (executeOps keys launches on it)
   const bool fold = p0.plan.ringColl == kTreeFlat;
+  // the small kernel holding only the exchange's transfers when every work of the launch needs
+  // no more (devcomm.h: kSetExchange)
+  int set = kSetExchange;
+  for (Planned* p : ps) {
+    const ncclComm* c = p->op.comm;
+    if (p->plan.ringColl != 0 || (size_t)p->plan.algoIndex >= c->algoSet.size() || c->algoSet[p->plan.algoIndex] != kSetExchange)
+      set = kSetAll;
+  }
   LaunchFn fn = fold ? getFoldLaunchFn(p0.plan.dtype, p0.op.devOp)
-                     : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp)
+                     : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp, set)
                              : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
-  for (Planned* p : ps) p->op.comm->last.small = fold ? 2 : small ? 1 : 0;
+  for (Planned* p : ps) {
+    p->op.comm->last.small = fold ? 2 : small ? 1 : 0;
+    p->op.comm->last.set = small ? set : 0;
+  }
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {
     // Every workgroup of the launch may spin on every other one (FIFO credits, dependency

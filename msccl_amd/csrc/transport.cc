@@ -582,7 +582,10 @@ bool sendCopyFusable(const Algorithm& a, const std::vector<Transfer>& ts, size_t
 // Pack every algorithm's per-tb programs into fixed-stride images and upload them (replaces
 // the 29 MB mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 ncclResult_t algoUpload(ncclComm* comm) {
+  comm->algoSet.assign(comm->algos.size(), kSetAll);
   for (size_t g = 0; g < comm->algos.size(); g++) {
+    // the small kernel variant its programs need (devcomm.h: kSetAll / kSetExchange)
+    bool exchangeOnly = true;
     const Algorithm& a = comm->algos[g];
     if (g >= comm->devAlgos.size()) comm->devAlgos.resize(g + 1);
     DevAlgoHost& d = comm->devAlgos[g];
@@ -611,8 +614,11 @@ ncclResult_t algoUpload(ncclComm* comm) {
       // one copy-send pass reads the source once.  A local change: the FIFO steps are the s's.
       for (size_t i = 0; comm->knobs.fuse && i + 1 < ts.size(); i++)
         if (sendCopyFusable(a, ts, i)) ts[i].type = kSendCopy;
+      for (const Transfer& t : ts)
+        if (t.type != kSend && t.type != kRecvReduceCopy && t.type != kSendRecvReduceCopy) exchangeOnly = false;
       putImage(img, (size_t)b * stride, h, ts, tb.depBid, tb.depStep, tb.redSrcOff);
     }
+    comm->algoSet[g] = exchangeOnly ? kSetExchange : kSetAll;
     NCCLCHECK(uploadImages(img, &d));
   }
   return ringUpload(comm);

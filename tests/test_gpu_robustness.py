@@ -177,3 +177,50 @@ def test_calls_beyond_2gib():
                         count, r, bad.shape[0], bad[:4].flatten().tolist()))
             del bufs, want
             torch.cuda.empty_cache()
+
+
+def _uneven_pair_xml(instances: int, extra: int) -> str:
+    """2-rank Simple pair exchange (s, rrc per thread block) where rank 0's thread blocks first run
+    `extra` local copies of their chunk into scratch: rank 0 produces late and rank 1's consumer
+    spins on the tail, its previous launch's loads of the same FIFO slots still in its caches."""
+    base = xmlgen.allreduce_pair_oneshot(instances, "Simple", max_bytes=1 << 24)
+    out = []
+    rank = None
+    for line in base.splitlines():
+        if line.strip().startswith("<gpu "):
+            rank = int(line.split('id="')[1].split('"')[0])
+            if rank == 0:
+                line = line.replace('s_chunks="0"', 's_chunks="%d"' % instances)
+        out.append(line)
+        if rank == 0 and line.strip().startswith("<tb "):
+            k = int(line.split('id="')[1].split('"')[0])
+            for _ in range(extra):
+                out.append('      <step s="0" type="cpy" srcbuf="i" srcoff="%d" dstbuf="s" dstoff="%d" cnt="1" '
+                           'depid="-1" deps="-1" hasdep="0"/>' % (k, k))
+    # renumber the steps of every thread block densely
+    text, res, s = "\n".join(out), [], 0
+    for line in text.splitlines():
+        if line.strip().startswith("<tb "):
+            s = 0
+        if line.strip().startswith("<step "):
+            line = line.split('s="')[0] + 's="%d"' % s + line.split('"', 2)[2][line.split('"', 2)[2].index(" "):]
+            s += 1
+        res.append(line)
+    return "\n".join(res) + "\n"
+
+
+def test_simple_handoff_uneven_load_l1_warm():
+    """The unfenced local Simple hand-off (sc0 sc1 stores drained, barrier, one
+    lane's tail post; the consumer polls the tail, then loads the slot after the barrier) under the
+    guide's hard case: uneven load (rank 0 does extra work before every send, so rank 1 waits on
+    the tail) and a consumer whose caches hold the same FIFO slots from the previous launch.  200
+    launches of an int32 Sum in place (every launch changes every word, a stale word cannot repeat
+    the expected value), every word of every launch checked against the oracle."""
+    from tests.gpu_harness import run_collective
+    xml = _uneven_pair_xml(8, 6)
+    algos = [L.parse_xml(xml, r, 2) for r in range(2)]
+    assert len(algos[0].tbs[0].transfers) == 8 and len(algos[1].tbs[0].transfers) == 2
+    # 8 chunks of 64 Ki int32: several 512-KiB FIFO slots per transfer
+    gpu, ora, _ = run_collective(xml, 2, L.ALLREDUCE, 8 * (1 << 16), 2, 0, True, seed=77, iters=200)
+    for r in range(2):
+        assert np.array_equal(gpu[r].view(np.uint32), ora[r].view(np.uint32)), describe_mismatch(gpu[r], ora[r])

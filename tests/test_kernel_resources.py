@@ -55,8 +55,10 @@ def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
     for k, v in fold.items():
         assert v.get("scratch", 1) == 0, (k, v)
     # the small-call kernel (fused exchange inside) for the same types and ops, both argument blocks
-    small = {k: v for k, v in ks.items() if re.search(r"mscclSmallKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi0ELi(2|16)EE", k)}
-    assert len(small) == 3 * 4 * 2, sorted(small)
+    # both transfer sets (devcomm.h: kSetAll, kSetExchange)
+    small = {k: v for k, v in ks.items()
+             if re.search(r"mscclSmallKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi0ELi(2|16)ELi[01]EE", k)}
+    assert len(small) == 3 * 4 * 2 * 2, sorted(small)
     for k, v in small.items():
         assert v.get("scratch", 1) == 0, (k, v)
 

@@ -10,6 +10,9 @@
 #   c345      the 8-rank C3 shape plus C4 / C5 (co-resident ranks)
 #   spawn     the 2-process launcher rehearsal on one GPU and the launcher's refusal
 #   sweep     bench.py sweeps of every library in LIBS (C2 2 ranks, then C3 shape 8 ranks fp16)
+#   xover     the lowered fold against the interpreter, 8 KiB - 128 KiB (MSCCL_AMD_LOWER_MAX_BYTES)
+#   c4trace   where the 8-rank C4 ring launch waits (tools/trace_report.py --summary)
+#   xcdpmc    rocprofv3's counter list and per-instance TCC request counters of the C2 launch
 # e.g. STEPS="suite lat" LIBS="tools/ab/a.so msccl_amd/libmsccl_amd.so" TAG=r04a bash tools/gpu_session.sh
 set -o pipefail
 export TMPDIR=/tmp
@@ -34,6 +37,36 @@ for step in $STEPS; do
         r=$(MSCCL_AMD_LIB=$L lat --schedule $1 --bytes $2 --ranks $3 --instances $4 --dtype $5) || fail "lat $L $spec"
         echo "$(basename $L) $r" | tee -a ${O}_lat.txt
       done
+    done ;;
+  xover)
+    # the fold (lowered) against the interpreter around MSCCL_AMD_LOWER_MAX_BYTES
+    for spec in "pair 2 16 7" "oneshot 8 4 6" "allpairs 8 1 6"; do
+      set -- $spec
+      for b in 8192 16384 32768 65536 131072; do
+        f=$(MSCCL_AMD_LOWER_MAX_BYTES=1073741824 lat --schedule $1 --bytes $b --ranks $2 --instances $3 --dtype $4) || fail "xover $spec $b"
+        i=$(MSCCL_AMD_LOWER=0 lat --schedule $1 --bytes $b --ranks $2 --instances $3 --dtype $4) || fail "xover $spec $b"
+        echo "fold: $f" | tee -a ${O}_xover.txt
+        echo "interp: $i" | tee -a ${O}_xover.txt
+      done
+    done ;;
+  c4trace)
+    MSCCL_AMD_TRACE=1 timeout -k 10 300 python3 tools/trace_report.py --schedule ring --ranks 8 --instances 32 --proto Simple \
+      --dtype 9 --bytes 268435456 --iters 3 --summary > ${O}_c4trace.txt 2>&1 || fail c4trace ${O}_c4trace.txt
+    cat ${O}_c4trace.txt ;;
+  xcdpmc)
+    # per-XCD memory requests of the C2 headline launch: the counters' dimensions, then one pass
+    # with the per-instance output kept (JSON)
+    timeout -s KILL 60 rocprofv3 -L > ${O}_counters.txt 2>&1 || fail "rocprofv3 -L" ${O}_counters.txt
+    for c in TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_HIT TCC_MISS; do
+      timeout -s KILL 120 rocprofv3 --pmc $c --output-format json csv -d gpurun_out/${TAG}_xcd_$c -o run -- \
+        python3 bench.py --sizes 33554432 --steps 10 --warmup 3 --no-cpu --quiet --no-secondary --pmc off --extras "" \
+        > /dev/null 2> ${O}_xcd_$c.err || fail "xcdpmc $c" ${O}_xcd_$c.err
+      # keep a summary and the head of the JSON (its per-dimension layout), not the raw output
+      d=gpurun_out/${TAG}_xcd_$c
+      { for f in $(find $d -name "*counter_collection.csv"); do head -3 $f; wc -l $f; done
+        for f in $(find $d -name "*.json"); do echo "== $f $(wc -c < $f) bytes"; head -c 150000 $f; echo; done
+      } > ${O}_xcd_$c.txt 2>&1
+      rm -rf $d
     done ;;
   trace)
     MSCCL_AMD_LIB=${LATLIB:-tools/ab/libmsccl_amd_lat.so} MSCCL_AMD_TRACE=2 timeout -k 5 90 python3 tools/lat_trace.py \
