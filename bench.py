@@ -154,8 +154,8 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
     minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
     ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
     for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
-    inst_large.  At more ranks: rank-ordered one-shot (4 instances) below 16 KiB, then two-phase
-    all-pairs, 1 instance below 64 KiB, inst_large above."""
+    inst_large.  At more ranks: rank-ordered one-shot (4 instances; lowered to the one-hop fold)
+    below 128 KiB, then two-phase all-pairs with inst_large instances."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
         # "O" = rank-ordered one-shot, "p" = 2-rank one-hop exchange (s, rrc), "r" = ring with
@@ -173,10 +173,12 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         # 32 MiB 398 -> 450 GB/s
         spec = [(0, 4 << 10, 1, "p"), (4 << 10, (1 << 30) + 1, inst_large, "p")]
     else:
-        # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 16 KiB: 8 ranks
-        # on one MI355X, fp16, 128 B 23.2 -> 19.5 us (profiles/r01_tier_sweep8.txt); it moves
-        # (n-1) S per rank, so the two-phase schedule takes over early
-        spec = [(0, 16 << 10, 4, "O"), (16 << 10, 64 << 10, 1), (64 << 10, (1 << 30) + 1, inst_large)]
+        # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 128 KiB: the
+        # runtime lowers it to the one-hop fold there (msccl_amd/csrc/lower.cc), which beats the
+        # two-phase all-pairs up to that size (8 ranks, fp16, graph replay: 16 KiB 18.8 -> 12.7 us,
+        # 64 KiB 23.1 -> 16.0, 128 KiB 24.2 -> 24.0; profiles/r04b_xover.txt); it moves (n-1) S per
+        # rank, so the two-phase schedule takes over above
+        spec = [(0, 128 << 10, 4, "O"), (128 << 10, (1 << 30) + 1, inst_large)]
     tiers = []
     for k, t in enumerate(spec):
         lo, hi, inst = t[:3]
@@ -765,14 +767,26 @@ def main():
         size_per = cnt // ncpl
         # the fused s + rrc pass runs only in mscclSmallKernel: the discount of one source read
         # applies to sizes whose launches ran there (comm info "last": the kernel of the last launch)
-        small = comms[0].info()["last"].get("small", 0) == 1
+        last = comms[0].info()["last"]
+        small = last.get("small", 0) == 1
+        lowered = last.get("small", 0) == 2   # the one-hop fold (msccl_amd/csrc/lower.cc)
         fz = fused.get(tier[3], ()) if small else ()
-        hbm, wire = schedule_bytes(algo, size_per, ts, proto_id, fused=fz)
-        payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True, fused=fz)
+        if lowered:
+            # the fold kernel: the input read once, LL lines to and from each of the n-1 peers,
+            # the result written
+            hbm = int(2 * nbytes + 2 * 2.0 * (n - 1) * nbytes)
+            wire = int(2.0 * (n - 1) * nbytes)
+            payload = int(2 * nbytes + 2 * (n - 1) * nbytes)
+        else:
+            hbm, wire = schedule_bytes(algo, size_per, ts, proto_id, fused=fz)
+            payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True, fused=fz)
         ok = verify(nbytes)
         verified.append(ok)
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
                         "payload_bytes_per_rank": payload, "verified": ok, "small": small,
+                        "kernel": ("mscclFoldKernel (lowered)" if lowered else
+                                   "mscclSmallKernel%s" % ("<exchange set>" if last.get("set") == 1 else "")
+                                   if small else "mscclKernel"),
                         "fused": bool(fz), "tier": tier[4],
                          "algbw": round(algbw, 3), "busbw": round(bus, 3),
                          "hbm_bytes_per_rank": hbm, "wire_bytes_per_rank": wire})
@@ -793,7 +807,7 @@ def main():
                      "payload_achieved counts them at payload size.  The launch's buffers (%d MiB, plus "
                      "FIFO slots) fit the 256 MB MALL, whose hits FETCH_SIZE counts: traffic is "
                      "memory-side bytes, not HBM-array bytes" % (head["bytes"] * ranks_on_gpu >> 20)),
-            "kernel": "%s<%s,Sum,%s>" % ("mscclSmallKernel" if headline_small else "mscclKernel", dtname, a.proto),
+            "kernel": "%s %s Sum %s" % (head["kernel"], dtname, a.proto),
             "algorithmic_bytes_per_launch": head["hbm_bytes_per_rank"] * ranks_on_gpu,
             "kernel_ms": head["kernel_ms"]}
     if multi and not one_gpu and world > 1:
@@ -873,7 +887,7 @@ def main():
                       "algbw_sum_gbs": round(head["bytes"] / (head["ms"] / 1e3) / 1e9 * n, 3)},
         "roofline": roof,
         "cpu_baseline": cpu,
-        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw", "verified", "small")} for r in results],
+        "sweep": [{k: r[k] for k in ("bytes", "ms", "kernel_ms", "busbw", "verified", "kernel")} for r in results],
     }
     if e2e:
         out["e2e"] = e2e

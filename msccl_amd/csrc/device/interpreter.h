@@ -460,6 +460,23 @@ struct Interp {
         la[2 * u + 1] = two[u] ? rslot + llLineIdx(q, 1) : la[2 * u];
       }
       ldLines8(la, ln);
+#ifdef MSCCL_EXP_BALLOT
+      // measurement build ("LL polls"): a wave-wide spin, every lane re-polling all
+      // its lines until no lane of the wave sees a stale flag
+      {
+        Spin spins;
+        while (true) {
+          bool stale = false;
+#pragma unroll
+          for (int u = 0; u < U; u++)
+            stale |= act[u] && (ln[2 * u].y != rflag || ln[2 * u].w != rflag || ln[2 * u + 1].y != rflag ||
+                                ln[2 * u + 1].w != rflag);
+          if (__builtin_amdgcn_ballot_w64(stale) == 0) break;
+          if (spinAbort(spins)) break;
+          ldLines8(la, ln);
+        }
+      }
+#endif
 #pragma unroll
       for (int u = 0; u < U; u++) {
         Spin spins;
@@ -958,8 +975,11 @@ struct Interp {
   // ---------------------------------------------------------------- launch prologue / epilogue
   // Prologue: one memory round trip.  The image (header + program), both connection records
   // and the launch epoch sit at addresses known from the block index, so all of them are in
-  // flight together: image by every lane with a 16-B unit, records by lanes 0-3 / 64-67 (other
-  // waves), the epoch by a lane of a third wave.  Returns the launch epoch (workIndex).
+  // flight together: the image by lane i for unit i (waves 0-5, kMaxImage16 units), the two
+  // records by lanes 448-455 (wave 7), the epoch by lane 384 (wave 6).  No wave issues two of
+  // them: a wave's LDS store waits for its load, and a second load behind it would be a second
+  // round trip (it was, for the image and the send record both in wave 0).  Returns the launch
+  // epoch (workIndex).
   __device__ __forceinline__ uint64_t prologue(const RankWork& w, int bid, int sub, DevTbHeader& hd) {
     tid = threadIdx.x;
     comm = w.comm;
@@ -970,12 +990,17 @@ struct Interp {
     const int slot = bid * w.maxSplit + sub;      // flag / epoch / trace slot of this workgroup
     const int cslot = bid * w.connSplit + sub;    // its connection records
     {
+      static_assert(kMaxImage16 <= 384, "image units must stay in waves 0-5");
       const u32x4* gimg = (const u32x4*)(w.images + (size_t)bid * w.tbStride);
       const int nU = w.tbStride >> 4;
-      for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
-      if (tid < 4) ((u32x4*)&sh->sconn)[tid] = ((const u32x4*)(w.send + cslot))[tid];
-      if (tid >= 64 && tid < 68) ((u32x4*)&sh->rconn)[tid - 64] = ((const u32x4*)(w.recv + cslot))[tid - 64];
-      if (tid == 128) {
+      if (tid < nU) sh->img[tid] = gimg[tid];
+      if (tid >= 448 && tid < 456) {
+        const int j = tid - 448;
+        const u32x4* src = j < 4 ? (const u32x4*)(w.send + cslot) + j : (const u32x4*)(w.recv + cslot) + (j - 4);
+        u32x4* dst = j < 4 ? (u32x4*)&sh->sconn + j : (u32x4*)&sh->rconn + (j - 4);
+        *dst = *src;
+      }
+      if (tid == 384) {
         sh->aborted = 0;
         sh->epoch = atomicLoadAgent(w.epochs + slot);
       }
@@ -1106,8 +1131,17 @@ struct Interp {
   }
 
   // ---------------------------------------------------------------- the interpreter loop
+  // Nothing before the prologue waits on a kernel argument or reads the clock: a stamp at entry
+  // (s_memrealtime is a scalar-memory op: the first wait for a kernel argument waits for it too)
+  // or a branch on an argument delayed the prologue's loads of every launch (the fold kernel:
+  // 0.5 us, profiles/r04c_lat.txt); the clock is read after the prologue, and only when traced.
   __device__ __forceinline__ void run(const RankWork& w, int bid, int sub) {
-    t0 = __builtin_amdgcn_s_memrealtime();
+    const int split = w.split;
+    const int maxSplit = w.maxSplit;
+    const int slot = bid * maxSplit + sub;
+    DevTbHeader hd;
+    const uint64_t workIndex = prologue(w, bid, sub, hd);
+    t0 = w.trace != nullptr || w.npkit != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
     redArg = w.redOpArg;
     if (w.redOpArgIsPtr) {  // ncclScalarDevice: the scale lives in device memory (enqueue.cc:1549-1557)
       T x;
@@ -1116,11 +1150,6 @@ struct Interp {
       __builtin_memcpy(&redArg, &x, sizeof(T));
       redArg = uni(redArg);
     }
-    const int split = w.split;
-    const int maxSplit = w.maxSplit;
-    const int slot = bid * maxSplit + sub;
-    DevTbHeader hd;
-    const uint64_t workIndex = prologue(w, bid, sub, hd);
     trace = w.trace ? w.trace + (size_t)slot * w.traceEvents : nullptr;
     nev = 1;
     maxEv = w.traceEvents;
@@ -1335,27 +1364,13 @@ struct Interp {
   // kernels keep their register budget.
   __device__ __forceinline__ void runFold(const RankWork& w, int wg, FoldShared* fs) {
     tid = threadIdx.x;
-    t0 = __builtin_amdgcn_s_memrealtime();
     comm = w.comm;
     timeoutTicks = w.timeoutTicks;
     llFlagMask = w.llFlagMask;
     llCleanMask = w.llCleanMask;
     redArg = 0;
-    // MSCCL_AMD_TRACE: the workgroup's setup, its one pass as one primitive, its end (slot wg);
-    // NPKit: the launch's time sync and the pass as one RECV_REDUCE_COPY_SEND (tb 0's buffer)
-    trace = w.trace ? w.trace + (size_t)wg * w.traceEvents : nullptr;
-    nev = 1;
-    maxEv = w.traceEvents;
+    trace = nullptr;  // set up after the prologue's loads are in flight (below)
     nkBuf = nullptr;
-    if (w.npkit != nullptr && wg == 0) {
-      const NpkitLog* lg = w.npkit;
-      nkCap = lg->cap;
-      nkBuf = lg->events;
-      nkHeadG = lg->heads;
-      nkHead = uni(*nkHeadG);
-      nk(NPKIT_EVENT_TIME_SYNC_CPU, 0, (uint64_t)(npkitTicksToNs(t0, lg->clockKHz) + lg->cpuOffsetNs));
-      nk(NPKIT_EVENT_TIME_SYNC_GPU, 0, t0);
-    }
     scG = nullptr;
     rcG = nullptr;
     const int np = w.foldPeers;
@@ -1377,6 +1392,8 @@ struct Interp {
     u32x4 pre = {0, 0, 0, 0};
     const bool havePre = w.ringColl != kRingReduceScatter && tid < npk;
     {
+      // issued first: the lane's later waits (for its image unit or record) then cover it too
+      if (havePre) pre = loadPack(srs, vec, p0 + tid, n);
       const u32x4* gimg = (const u32x4*)w.images;
       const int nU = w.tbStride >> 4;
       for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
@@ -1392,10 +1409,28 @@ struct Interp {
         sh->aborted = 0;
         sh->epoch = atomicLoadAgent(w.epochs + wg);  // slot wg of the fold's range
       }
-      if (havePre) pre = loadPack(srs, vec, p0 + tid, n);
     }
     __syncthreads();
     const uint64_t workIndex = uni(sh->epoch);
+    // MSCCL_AMD_TRACE: the workgroup's setup, its one pass as one primitive, its end (slot wg);
+    // NPKit: the launch's time sync and the pass as one RECV_REDUCE_COPY_SEND (tb 0's buffer).
+    // After the prologue: the kernel-argument loads these branches chain would otherwise delay the
+    // prologue's loads (0.4-0.7 us per launch, profiles/r04b_lat.txt)
+    t0 = w.trace != nullptr || w.npkit != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (w.trace != nullptr) {
+      trace = w.trace + (size_t)wg * w.traceEvents;
+      nev = 1;
+      maxEv = w.traceEvents;
+    }
+    if (w.npkit != nullptr && wg == 0) {
+      const NpkitLog* lg = w.npkit;
+      nkCap = lg->cap;
+      nkBuf = lg->events;
+      nkHeadG = lg->heads;
+      nkHead = uni(*nkHeadG);
+      nk(NPKIT_EVENT_TIME_SYNC_CPU, 0, (uint64_t)(npkitTicksToNs(t0, lg->clockKHz) + lg->cpuOffsetNs));
+      nk(NPKIT_EVENT_TIME_SYNC_GPU, 0, t0);
+    }
     DevTbHeader hd;
     {
       u32x4 raw = sh->img[0];
@@ -1605,7 +1640,9 @@ struct Interp {
   // big loop keeps live (SGPR spills), a few us per launch.
   template <int SET>
   __device__ __forceinline__ void runSmall(const RankWork& w, int local) {
-    const uint64_t tStart = w.trace ? __builtin_amdgcn_s_memrealtime() : 0;  // MSCCL_AMD_TRACE=2
+#ifdef MSCCL_LAT_TRACE
+    const uint64_t tStart = __builtin_amdgcn_s_memrealtime();  // the measurement build's time origin
+#endif
     redArg = 0;
     trace = nullptr;
     nkBuf = nullptr;
@@ -1614,6 +1651,10 @@ struct Interp {
     const int bid = local >> lg, sub = local & (split - 1);
     DevTbHeader hd;
     const uint64_t workIndex = prologue(w, bid, sub, hd);
+#ifndef MSCCL_LAT_TRACE
+    // MSCCL_AMD_TRACE=2's start stamp: after the prologue (see run())
+    const uint64_t tStart = w.trace != nullptr ? __builtin_amdgcn_s_memrealtime() : 0;
+#endif
     const int maxSplit = w.maxSplit;
 #ifdef MSCCL_LAT_TRACE
     trace = w.trace ? w.trace + (size_t)(bid * maxSplit + sub) * w.traceEvents : nullptr;
@@ -1725,12 +1766,23 @@ struct Interp {
   }
 };
 
+// The rank of the launch that owns block b: ranks' blocks are consecutive ([blockBase, blockBase +
+// nBlocks) in rank order), so r = the number of ranks i >= 1 whose blocks start at or below b.  All
+// R block bases are independent kernel-argument loads issued together (a search loop over them
+// was one dependent scalar load per rank before the prologue could start).
+template <int R>
+__device__ __forceinline__ int rankOfBlock(const LaunchArgsN<R>& args, int b) {
+  int r = 0;
+#pragma unroll
+  for (int i = 1; i < R; i++) r += (i < args.nRanks && b >= args.w[i].blockBase) ? 1 : 0;
+  return r;
+}
+
 template <typename T, int OP, int PROTO>
 __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
   __shared__ BlockShared sh;
-  int b = blockIdx.x;
-  int r = 0;
-  while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
+  const int b = blockIdx.x;
+  const int r = rankOfBlock(args, b);
   const RankWork& w = args.w[r];
   const int local = b - w.blockBase;
   Interp<T, OP, PROTO> it;
@@ -1743,9 +1795,8 @@ __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
 template <typename T, int OP, int PROTO, int R, int SET>
 __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> args) {
   __shared__ BlockShared sh;
-  int b = blockIdx.x;
-  int r = 0;
-  while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
+  const int b = blockIdx.x;
+  const int r = rankOfBlock(args, b);
   const RankWork& w = args.w[r];
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
@@ -1759,8 +1810,7 @@ __global__ void __launch_bounds__(kNT, 1) mscclFoldKernel(const LaunchArgsN<R> a
   __shared__ BlockShared sh;
   __shared__ FoldShared fs;
   const int b = blockIdx.x;
-  int r = 0;
-  while (r < args.nRanks - 1 && b >= args.w[r].blockBase + args.w[r].nBlocks) r++;
+  const int r = rankOfBlock(args, b);
   Interp<T, OP, pLL> it;
   it.sh = &sh;
   it.runFold(args.w[r], b - args.w[r].blockBase, &fs);

@@ -46,7 +46,9 @@ ncclResult_t loadAlgos(ncclComm* comm) {
 // then keeps a lowering only where every rank reached it (applySplits).
 void analyzeLowering(ncclComm* comm) {
   comm->algoFoldOrder.assign(comm->algos.size(), {});
-  if (!comm->knobs.lower || !flatEnabled(comm)) return;
+  // NPKit logs the schedule's own primitives (msccl_interpreter.h's placement): a rank with the
+  // log on offers no lowering, and the init allgather then keeps the interpreter on every rank
+  if (!comm->knobs.lower || !flatEnabled(comm) || envInt("MSCCL_AMD_NPKIT", 0) > 0) return;
   for (size_t g = 0; g < comm->algos.size(); g++) {
     const Algorithm& a = comm->algos[g];
     if (!a.valid || a.coll != kAllReduce || a.proto != kProtoLL || a.path.empty()) continue;

@@ -82,7 +82,7 @@ Knobs Knobs::fromEnv() {
   k.fuse = envInt("MSCCL_AMD_FUSE", 1) != 0;
   k.treeFlat = envInt("MSCCL_AMD_TREE_FLAT", 1) != 0;
   k.lower = envInt("MSCCL_AMD_LOWER", 1) != 0;
-  k.lowerMaxBytes = envInt("MSCCL_AMD_LOWER_MAX_BYTES", 32 << 10);
+  k.lowerMaxBytes = envInt("MSCCL_AMD_LOWER_MAX_BYTES", -1);  // -1: by rank count (lowerToFoldPlan)
   return k;
 }
 
@@ -283,7 +283,12 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
 }
 
 int lowerToFoldPlan(const CallDesc& c, const Knobs& k, Plan* p) {
-  if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > k.lowerMaxBytes ||
+  // Where the fold beats the interpreted schedule (co-resident ranks, graph replay,
+  // profiles/r04b_xover.txt): 2 ranks up to a few KiB (the exchange-set kernel runs the pair
+  // exchange itself in ~6.6 us from 8 KiB on), 8 ranks up to 128 KiB (the one-shot 16 KiB 20.2 ->
+  // 12.7 us, 64 KiB 23.9 -> 16.0; the two-phase all-pairs 18.8 / 23.1 there)
+  const int64_t limit = k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : c.nRanks <= 2 ? (int64_t)(4 << 10) : (int64_t)(128 << 10);
+  if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > limit ||
       p->nBytes > (1ll << 30))
     return 1;
   // the fold kernel's chunk math (makeFlatTreePlan): one call over the whole buffer

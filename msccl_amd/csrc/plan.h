@@ -77,7 +77,7 @@ struct Knobs {
   int32_t treeFlat;          // MSCCL_AMD_TREE_FLAT: the tree's values in one hop (plan.cc: makeFlatTreePlan)
   int32_t lower;             // MSCCL_AMD_LOWER: one-hop AllReduce schedules run as the fold (lower.cc)
   int32_t pad0;
-  int64_t lowerMaxBytes;     // MSCCL_AMD_LOWER_MAX_BYTES: largest call (bytes per rank) lowered
+  int64_t lowerMaxBytes;     // MSCCL_AMD_LOWER_MAX_BYTES: largest call (bytes per rank) lowered (-1: by ranks)
   static Knobs fromEnv();
 };
 

@@ -40,6 +40,7 @@ def _run(cr, count, dt, op, seed):
 @pytest.mark.parametrize("count,dt,op", [(64, 7, 0), (320, 7, 2), (192, 7, 0), (1024, 6, 0), (16384, 9, 0),
                                          (8192, 7, 3)])
 def test_small_kernel_matches_oracle_and_general(name, count, dt, op, tmp_path, monkeypatch):
+    monkeypatch.setenv("MSCCL_AMD_LOWER", "0")   # the interpreter kernels, not the one-hop fold
     n, gen = SCHEDULES[name]
     xml = gen()
     xp = tmp_path / "s.xml"
