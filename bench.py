@@ -51,7 +51,9 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--e2e", action="store_true", help="also time H2D + AllReduce + D2H")
-    ap.add_argument("--graph", action="store_true", help="time the K steps as one captured hipGraph replay")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch the K timed steps one by one from Python (default: capture them into one hipGraph "
+                         "and time its replay, as the reference's nccl-tests run does with -G 100, README.md:57)")
     ap.add_argument("--extras", default=None,
                     help="also measure C4 (ring Simple bf16 256 MiB) / C5 (RS+AG fp32 64 MiB), e.g. C4,C5 "
                          "(default: both when 8 ranks run one per GPU)")
@@ -568,7 +570,7 @@ def live_pmc(a, timeout_s: int = 150):
     if prof is None:
         return None, "rocprofv3 not found"
     child = [sys.executable, os.path.abspath(__file__), "--sizes", "33554432", "--steps", "10", "--warmup", "3",
-             "--no-cpu", "--quiet", "--no-secondary", "--pmc", "off", "--extras", "",
+             "--no-cpu", "--quiet", "--no-secondary", "--pmc", "off", "--extras", "", "--eager",
              "--vranks", str(a.vranks), "--proto", a.proto]
     if a.dtype:
         child += ["--dtype", a.dtype]
@@ -731,13 +733,17 @@ def main():
         for _ in range(a.warmup):
             one_step(nbytes)
         graph = None
-        if a.graph:
-            # nccl-tests -G style: the K timed steps captured once into a hipGraph, replayed once
+        if not a.eager:
+            # nccl-tests -G style (the reference's run, README.md:57): the K timed steps captured
+            # once into a hipGraph; one untimed replay uploads it, the timed one replays the K steps
             torch.cuda.synchronize()
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
                 for _ in range(a.steps):
                     one_step(nbytes)
+            with torch.cuda.stream(stream):
+                graph.replay()
+            torch.cuda.synchronize()
         barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -875,7 +881,7 @@ def main():
                    "instances_large": inst, "proto": a.proto, "sweep_bytes": [sizes[0], sizes[-1]],
                    "tiers": [[t[0], t[1], t[2], {"a": "allpairs", "o": "oneshot", "O": "oneshot-ordered",
                                                  "p": "pair-oneshot", "r": "ring"}[t[4]]] for t in tiers],
-                   "launch": "hipgraph" if a.graph else "eager",
+                   "launch": "eager" if a.eager else "hipgraph (K steps captured, replayed once)",
                    "knobs": knobs},
         "avg_busbw": round(float(np.mean([r["busbw"] for r in results])), 3),
         "verified": bool(verified) and all(verified),

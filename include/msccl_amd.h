@@ -27,8 +27,9 @@ int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, si
 
 /* Whether the AllReduce schedule of one MSCCL XML file, loaded for every rank of `nranks`, runs as
  * the one-hop fold (msccl_amd/csrc/lower.cc: every result chunk of every rank is a left fold of all
- * ranks' same chunk in one order per rank).  JSON {"ok":1,"order":[[ranks of rank 0's fold], ...]}
- * or {"ok":0,"why":"..."}.  No GPU needed. */
+ * ranks' same chunk; chunks fall into classes of equal orders).  JSON {"ok":1,"classes":[[[ranks of
+ * rank 0's fold], ... per rank], ... per class],"chunkClass":[class of chunk 0, ...]} or
+ * {"ok":0,"why":"..."}.  No GPU needed. */
 int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen);
 
 /* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the launch plan

@@ -151,7 +151,8 @@ def fusable_json(xml_path: str, rank: int, nranks: int, key: str = "fusable") ->
 
 def lower_json(xml_path: str, nranks: int) -> dict:
     """Whether the AllReduce schedule runs as the one-hop fold kernel (msccl_amd/csrc/lower.cc):
-    {"ok": 1, "order": [fold order of rank 0, ...]} or {"ok": 0, "why": reason}."""
+    {"ok": 1, "classes": [[fold order of rank 0, ...] per class of chunks], "chunkClass": [class of
+    each chunk]} or {"ok": 0, "why": reason}."""
     buf = ctypes.create_string_buffer(1 << 16)
     _check(lib().mscclAmdLowerJson(xml_path.encode(), nranks, buf, len(buf)), "mscclAmdLowerJson")
     return json.loads(buf.value.decode())

@@ -73,7 +73,11 @@ struct ncclComm {
   std::vector<msccl::DevAlgoHost> devAlgos;
   // per algorithm: this rank's fold order when the schedule runs as the one-hop fold (lower.cc;
   // empty: it does not) and the fold kernel's program for it (nBlocks 0 when empty)
-  std::vector<std::vector<int>> algoFoldOrder;
+  struct FoldProgram {
+    std::vector<int> chunkClass;            // class of every chunk (lower.h)
+    std::vector<std::vector<int>> order;    // this rank's fold order (ranks) per class; empty: not lowered
+  };
+  std::vector<FoldProgram> algoFold;
   std::vector<int> algoSet;  // per algorithm: the small kernel's transfer set (transport.cc: algoUpload)
   std::vector<msccl::DevAlgoHost> foldAlgos;
   msccl::DevAlgoHost ringAlgos[6];  // ring fallback programs, [4] = tree, [5] = flat tree (transport.cc: ringUpload)

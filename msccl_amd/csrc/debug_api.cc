@@ -65,12 +65,19 @@ int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen)
   std::ostringstream o;
   o << "{\"ok\":" << (fl.ok ? 1 : 0);
   if (fl.ok) {
-    o << ",\"order\":[";
-    for (size_t r = 0; r < fl.order.size(); r++) {
-      o << (r ? "," : "") << "[";
-      for (size_t i = 0; i < fl.order[r].size(); i++) o << (i ? "," : "") << fl.order[r][i];
+    // "classes": per class of chunks, every rank's fold order; "chunkClass": every chunk's class
+    o << ",\"classes\":[";
+    for (size_t k = 0; k < fl.order.size(); k++) {
+      o << (k ? "," : "") << "[";
+      for (size_t r = 0; r < fl.order[k].size(); r++) {
+        o << (r ? "," : "") << "[";
+        for (size_t i = 0; i < fl.order[k][r].size(); i++) o << (i ? "," : "") << fl.order[k][r][i];
+        o << "]";
+      }
       o << "]";
     }
+    o << "],\"chunkClass\":[";
+    for (size_t c = 0; c < fl.chunkClass.size(); c++) o << (c ? "," : "") << fl.chunkClass[c];
     o << "]";
   } else {
     o << ",\"why\":\"" << fl.why << "\"";

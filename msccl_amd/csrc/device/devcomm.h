@@ -37,6 +37,8 @@ constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
 constexpr int kMaxFoldPeers = 15;      // flat tree fold: peers of one rank (MSCCL_MAX_REDUCE_FUSION 16 ranks)
 constexpr int kFlatSubs = 4;           // flat tree: sub-connections per peer = most fold workgroups per rank
 constexpr int kFoldPacksPerWg = 512;   // flat tree: a fold workgroup per 512 packs (8 KiB) of the call
+constexpr int kMaxFoldClasses = 16;    // lowered schedules (lower.cc): fold orders per schedule
+constexpr int kMaxFoldChunks = 1024;   // lowered schedules with several orders: chunks per loop
 
 // Device trace event (mscclAmdTraceRead).
 struct TraceEvent {
@@ -203,6 +205,7 @@ struct RankWork {
   // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)
   uint8_t ringColl;
   int16_t ringRanks;
+  int32_t foldChunkPacks;       // a lowered schedule folding chunks in several orders: packs per chunk (else 0)
   int64_t ringSize;             // elements of one rank's block (args->count)
   int64_t ringLastChunk;        // LL ReduceScatter / AllGather lastChunkSize (enqueue.cc:653-658)
   // copies of per-communicator constants (kernel arguments: no dependent DevComm load)

@@ -57,6 +57,11 @@ struct alignas(16) FoldShared {
     uint32_t sflag, rflag;
   } fold[kMaxFoldPeers];
   uint8_t perm[kMaxFoldPeers + 1];  // peer record of each fold position (the own input skipped)
+  // a lowered schedule folding its chunks in several orders (lower.cc: classes): per class the
+  // peer record of each fold position and the position of the own input; the class of each chunk
+  uint8_t cperm[kMaxFoldClasses][kMaxFoldPeers + 1];
+  uint8_t cown[kMaxFoldClasses];
+  uint8_t chunkClass[kMaxFoldChunks];
 };
 
 __device__ __forceinline__ uint64_t computeFlag(uint64_t workIndex, uint64_t iter, uint64_t step) {
@@ -1456,6 +1461,24 @@ struct Interp {
         nq++;
       }
     }
+    // several orders (w.foldChunkPacks = packs per chunk > 0): transfer 3 holds every class's
+    // order, transfer 4 every chunk's class (transport.cc: foldImage); a pack folds in its chunk's
+    // order (read after the first step's barrier, like perm)
+    const int cpk = w.foldChunkPacks;
+    if (cpk > 0) {
+      const DevTransfer t3 = loadTransfer(tr0 + 3), t4 = loadTransfer(tr0 + 4);
+      const int16_t* co = reds + t3.redPtr;
+      for (int i = tid; i < t3.srcoff; i += kNT) {  // one lane per class
+        int q = 0;
+        for (int j = 0; j < nfold; j++) {
+          const int b = co[i * nfold + j];
+          if (b < 0) fs->cown[i] = (uint8_t)q;
+          else fs->cperm[i][q++] = (uint8_t)(b - 1);
+        }
+      }
+      const int16_t* cc = reds + t4.redPtr;
+      for (int i = tid; i < t4.srcoff; i += kNT) fs->chunkClass[i] = (uint8_t)cc[i];
+    }
     const int slotLines = uni(fs->foldRecv[0].llSlotLines);
     const int slotPacks = slotLines / 2;
     ev(kEvSetup, 0, 0);
@@ -1545,12 +1568,20 @@ struct Interp {
         }
         u32x4 acc = (u32x4){0, 0, 0, 0};
         bool first = true;
+        // this pack's fold order: the schedule's one, or its chunk's class's (per lane)
+        const uint8_t* pm = fs->perm;
+        int ownPos = ownAt;
+        if (cpk > 0) {
+          const int cls = fs->chunkClass[B / cpk];
+          pm = fs->cperm[cls];
+          ownPos = fs->cown[cls];
+        }
         for (int g0 = 0; g0 < nq; g0 += G) {  // the fold, peers in fold order
           const void* la[2 * G];
           int pk[G];
 #pragma unroll
           for (int k = 0; k < G; k++) {
-            pk[k] = fs->perm[g0 + k < nq ? g0 + k : g0];
+            pk[k] = pm[g0 + k < nq ? g0 + k : g0];
             const char* in = (const char*)fs->fold[pk[k]].in;
             la[2 * k] = in + o0;
             la[2 * k + 1] = in + o1;
@@ -1561,7 +1592,7 @@ struct Interp {
           for (int k = 0; k < G; k++) {
             const int p = g0 + k;
             if (p >= nq) continue;
-            if (p == ownAt) {
+            if (p == ownPos) {
               acc = first ? own : F::pack(acc, own);
               first = false;
             }
@@ -1577,7 +1608,7 @@ struct Interp {
             first = false;
           }
         }
-        if (ownAt == nq) acc = first ? own : F::pack(acc, own);
+        if (ownPos == nq) acc = first ? own : F::pack(acc, own);
         storePack(drs, vec, B, n, acc);
       }
       for (int k = 0; k < np; k++) {

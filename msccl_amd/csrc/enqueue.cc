@@ -122,8 +122,8 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
     protoOverride = kProtoLL;
   }
   NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, comm->knobs, &out->plan));
-  if ((size_t)idx < comm->algoFoldOrder.size() && !comm->algoFoldOrder[idx].empty() && flatEnabled(comm) &&
-      lowerToFoldPlan(c, comm->knobs, &out->plan) == 0) {
+  if ((size_t)idx < comm->algoFold.size() && !comm->algoFold[idx].order.empty() && flatEnabled(comm) &&
+      lowerToFoldPlan(c, comm->knobs, (int)comm->algoFold[idx].order.size(), &out->plan) == 0) {
     // a one-hop schedule (lower.cc): the fold kernel computes its values in one hop
     INFO(kSubColl, "MSCCL: %s count=%zu runs as the one-hop fold", comm->algos[idx].name.c_str(), op.count);
     return ncclSuccess;
@@ -240,6 +240,7 @@ RankWork makeFlatWork(Planned& p) {
   // the kernel's collective: 0 the flat tree's AllReduce, else kRingReduceScatter / kRingAllGather
   w.ringColl = (uint8_t)(p.plan.flatColl == kRingAllReduce ? 0 : p.plan.flatColl);
   w.foldPeers = (uint8_t)(comm->nRanks - 1);
+  w.foldChunkPacks = (int32_t)p.plan.foldChunkPacks;
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
   w.launchSeq = comm->workIndex++;

@@ -45,7 +45,7 @@ ncclResult_t loadAlgos(ncclComm* comm) {
 // rank of the communicator (as each of them loads it) and decides the same; the init allgather
 // then keeps a lowering only where every rank reached it (applySplits).
 void analyzeLowering(ncclComm* comm) {
-  comm->algoFoldOrder.assign(comm->algos.size(), {});
+  comm->algoFold.assign(comm->algos.size(), ncclComm::FoldProgram());
   // NPKit logs the schedule's own primitives (msccl_interpreter.h's placement): a rank with the
   // log on offers no lowering, and the init allgather then keeps the interpreter on every rank
   if (!comm->knobs.lower || !flatEnabled(comm) || envInt("MSCCL_AMD_NPKIT", 0) > 0) return;
@@ -60,7 +60,11 @@ void analyzeLowering(ncclComm* comm) {
     }
     if (!loaded) continue;
     const FoldLowering fl = analyzeFoldLowering(byRank);
-    if (fl.ok) comm->algoFoldOrder[g] = fl.order[comm->rank];
+    if (fl.ok) {
+      ncclComm::FoldProgram& f = comm->algoFold[g];
+      f.chunkClass = fl.chunkClass;
+      for (auto& perRank : fl.order) f.order.push_back(perRank[comm->rank]);
+    }
     INFO(kSubInit, "MSCCL: algorithm %s %s", a.name.c_str(),
          fl.ok ? "is a one-hop fold: calls up to MSCCL_AMD_LOWER_MAX_BYTES run the fold kernel"
                : ("runs interpreted (" + fl.why + ")").c_str());
@@ -136,7 +140,7 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) {
     s.nBlocks[a] = comm->algos[a].nBlocks;
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
-    s.lowered[a] = a < comm->algoFoldOrder.size() && !comm->algoFoldOrder[a].empty();
+    s.lowered[a] = a < comm->algoFold.size() && !comm->algoFold[a].order.empty();
     const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
     for (size_t i = 0; i < fc.size() && s.nFuse[a] < kMaxFuse; i++) {
       s.fuse[a][s.nFuse[a]][0] = fc[i].chan;
@@ -218,9 +222,9 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   }
   // a schedule runs as the fold only when every rank found it one (the two ends of every flat
   // connection must run the same kernel)
-  for (size_t a = 0; a < comm->algoFoldOrder.size() && a < (size_t)kMaxAlgos; a++)
+  for (size_t a = 0; a < comm->algoFold.size() && a < (size_t)kMaxAlgos; a++)
     for (auto& r : recs)
-      if ((int)a >= r.nAlgos || !r.lowered[a]) comm->algoFoldOrder[a].clear();
+      if ((int)a >= r.nAlgos || !r.lowered[a]) comm->algoFold[a] = ncclComm::FoldProgram();
   // an exchange runs fused only when both ends offered it (fusableTbs)
   comm->algoFuse.assign(comm->algos.size(), {});
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos && comm->knobs.fuse; a++) {

@@ -89,6 +89,7 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
     out.ok = false;
     out.why = why;
     out.order.clear();
+    out.chunkClass.clear();
     return out;
   };
   if (n < 2 || n > kMaxReduceFusion) return fail("ranks outside 2..16");
@@ -224,8 +225,8 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
       if (st[r][b].pc < byRank[r].tbs[b].transfers.size()) return fail("schedule does not complete");
   for (auto& kv : fifo)
     if (!kv.second.empty()) return fail("unconsumed FIFO messages");
-  // every result chunk: a left fold of all ranks' same chunk, one order per rank
-  out.order.assign(n, {});
+  // every result chunk: a left fold of all ranks' same chunk; orders per (chunk, rank)
+  std::vector<std::vector<std::vector<int>>> ordOf(C, std::vector<std::vector<int>>(n));
   for (int r = 0; r < n; r++) {
     const std::vector<int>& res = byRank[r].inPlace ? inB[r] : outB[r];
     if (!byRank[r].inPlace)
@@ -261,10 +262,21 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
         ranks.push_back(q);
       }
       if ((int)ranks.size() != n) return fail("a result chunk misses a rank");
-      if (c == 0) out.order[r] = ranks;
-      else if (ranks != out.order[r]) return fail("the fold order differs between chunks of one rank");
+      ordOf[c][r] = ranks;
     }
   }
+  // classes: chunks whose orders agree on every rank
+  out.chunkClass.assign(C, -1);
+  for (int c = 0; c < C; c++) {
+    for (size_t k = 0; k < out.order.size() && out.chunkClass[c] < 0; k++)
+      if (out.order[k] == ordOf[c]) out.chunkClass[c] = (int)k;
+    if (out.chunkClass[c] < 0) {
+      out.chunkClass[c] = (int)out.order.size();
+      out.order.push_back(ordOf[c]);
+    }
+  }
+  if ((int)out.order.size() > kMaxFoldClasses) return fail("more fold orders than the fold kernel holds");
+  if (out.order.size() > 1 && C > kMaxFoldChunks) return fail("more chunks than the fold kernel's class map holds");
   out.ok = true;
   return out;
 }

@@ -8,14 +8,18 @@
 namespace msccl {
 
 // byRank[r]: the schedule as loaded for rank r (every rank of the communicator).  ok: on every
-// rank r every result chunk c is x_{order[r][0]}[c] (+) x_{order[r][1]}[c] (+) ... (+)
-// x_{order[r][n-1]}[c] (a left fold over all ranks, one order per rank) under the LL protocol's
-// semantics, so the flat fold kernel with that order computes the schedule's values; why: the
-// reason it is not.
+// rank r every result chunk c is a left fold over all ranks of their chunk c,
+// x_{o(0)}[c] (+) x_{o(1)}[c] (+) ... (+) x_{o(n-1)}[c], under the LL protocol's semantics, so the
+// flat fold kernel with those orders computes the schedule's values; why: the reason it is not.
+// The chunks fall into classes of identical orders on every rank (a one-shot: one class; the
+// two-phase all-pairs: one per chunk owner, who folds its own chunk first):
+//   chunkClass[c]       the class of chunk c (classes numbered by their first chunk);
+//   order[k][r]         the fold order (ranks) of class k on rank r.
 struct FoldLowering {
   bool ok = false;
   std::string why;
-  std::vector<std::vector<int>> order;
+  std::vector<int> chunkClass;
+  std::vector<std::vector<std::vector<int>>> order;
 };
 FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank);
 

@@ -282,7 +282,7 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   return 0;
 }
 
-int lowerToFoldPlan(const CallDesc& c, const Knobs& k, Plan* p) {
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p) {
   // Where the fold beats the interpreted schedule (co-resident ranks, graph replay,
   // profiles/r04b_xover.txt): 2 ranks up to a few KiB (the exchange-set kernel runs the pair
   // exchange itself in ~6.6 us from 8 KiB on), 8 ranks up to 128 KiB (the one-shot 16 KiB 20.2 ->
@@ -291,8 +291,11 @@ int lowerToFoldPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > limit ||
       p->nBytes > (1ll << 30))
     return 1;
-  // the fold kernel's chunk math (makeFlatTreePlan): one call over the whole buffer
   const int ts = refTypeSize(p->dtype);
+  const int64_t pe = 16 / ts;
+  if (classes > 1 && (p->sizePerChunk % pe != 0 || p->nchunksPerLoop > kMaxFoldChunks)) return 1;
+  p->foldChunkPacks = classes > 1 ? p->sizePerChunk / pe : 0;
+  // the fold kernel's chunk math (makeFlatTreePlan): one call over the whole buffer
   const int64_t stepSize = k.buffSizes[kProtoLL] / kFifoSteps;
   p->ringColl = kTreeFlat;
   p->flatColl = kRingAllReduce;

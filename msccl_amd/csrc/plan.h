@@ -49,6 +49,8 @@ struct Plan {
   // ringColl == kTreeFlat: the collective the fold kernel runs (kRingAllReduce for the flat tree,
   // kRingReduceScatter / kRingAllGather for the flat forms of the ring's)
   int flatColl = 0;
+  // a lowered schedule with several fold orders (lowerToFoldPlan): 16-B packs per chunk, else 0
+  int64_t foldChunkPacks = 0;
 };
 
 // Every environment knob the per-call planning reads, captured once at communicator init
@@ -115,6 +117,8 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p);
 // Sum..Min, at most MSCCL_AMD_LOWER_MAX_BYTES per rank): turns the schedule's plan into the fold
 // kernel's (ringColl kTreeFlat, flatColl kRingAllReduce; algoIndex kept: the fold runs with the
 // schedule's own fold order, ncclComm::foldAlgos).  Returns 0, or nonzero (plan unchanged).
-int lowerToFoldPlan(const CallDesc& c, const Knobs& k, Plan* p);
+// classes: the schedule's fold orders (lower.h); with several, the call's chunks must be whole
+// 16-B packs (each pack folds in its chunk's order).
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p);
 
 }  // namespace msccl

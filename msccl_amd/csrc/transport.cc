@@ -467,10 +467,15 @@ ncclResult_t ringUpload(ncclComm* comm) {
         if (rp[b] == q) return b;
       return -1;
     };
-    // arOrder: the AllReduce's fold order (ranks); the flat tree's is n-1 .. 0, a lowered
-    // schedule's its own (lower.cc)
-    auto foldImage = [&](const std::vector<int>& arOrder, DevAlgoHost& d) -> ncclResult_t {
+    // The AllReduce's fold orders (ranks): the flat tree's is n-1 .. 0 (one class); a lowered
+    // schedule's are its own (lower.cc), one per class of chunks.  Tables in the image's reduction
+    // list, one transfer each (positions map to peer records, -1 = this rank's input):
+    //   0: the AllReduce fold order of class 0; 1: the ReduceScatter order; 2: the rank of every
+    //   peer record, then this rank; with several classes also 3: every class's order (srcoff =
+    //   classes) and 4: the class of every chunk (srcoff = chunks).
+    auto foldImage = [&](const ncclComm::FoldProgram& fp, DevAlgoHost& d) -> ncclResult_t {
     std::vector<int16_t> reds;
+    const std::vector<int>& arOrder = fp.order[0];
     for (int q : arOrder) reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
     for (int i = 1; i <= n; i++) {
       const int q = (r + i) % n;
@@ -478,7 +483,8 @@ ncclResult_t ringUpload(ncclComm* comm) {
     }
     for (int b = 1; b < n; b++) reds.push_back((int16_t)rp[b]);
     reds.push_back((int16_t)r);
-    std::vector<Transfer> ts(3);
+    const bool multi = fp.order.size() > 1;
+    std::vector<Transfer> ts(multi ? 5 : 3);
     for (int i = 0; i < 3; i++) {
       ts[i].type = kFoldRecv;
       ts[i].srcbuf = kInput;
@@ -486,6 +492,17 @@ ncclResult_t ringUpload(ncclComm* comm) {
       ts[i].count = 1;
       ts[i].numReds = (int16_t)n;
       ts[i].redPtr = (int16_t)(i * n);
+    }
+    if (multi) {
+      ts[3] = ts[0];
+      ts[3].redPtr = (int16_t)reds.size();
+      ts[3].srcoff = (int16_t)fp.order.size();
+      for (const std::vector<int>& o : fp.order)
+        for (int q : o) reds.push_back((int16_t)(q == r ? -1 : tbOf(q)));
+      ts[4] = ts[0];
+      ts[4].redPtr = (int16_t)reds.size();
+      ts[4].srcoff = (int16_t)fp.chunkClass.size();
+      for (int k : fp.chunkClass) reds.push_back((int16_t)k);
     }
     d.nBlocks = 1;
     d.tbStride = (int)imageBytes(ts.size(), 0, reds.size());
@@ -501,14 +518,15 @@ ncclResult_t ringUpload(ncclComm* comm) {
     putImage(img, 0, h, ts, none, none, reds);
     return uploadImages(img, &d);
     };
-    std::vector<int> chain;
-    for (int q = n - 1; q >= 0; q--) chain.push_back(q);
+    ncclComm::FoldProgram chain;
+    chain.order.emplace_back();
+    for (int q = n - 1; q >= 0; q--) chain.order[0].push_back(q);
     NCCLCHECK(foldImage(chain, comm->ringAlgos[5]));
-    // the one-hop MSCCL schedules (lower.cc): the fold with the schedule's order, over the same
+    // the one-hop MSCCL schedules (lower.cc): the fold with the schedule's orders, over the same
     // flat connections (the step counters are the connections', whichever program runs)
     comm->foldAlgos.assign(comm->algos.size(), DevAlgoHost());
-    for (size_t g = 0; g < comm->algoFoldOrder.size(); g++)
-      if (!comm->algoFoldOrder[g].empty()) NCCLCHECK(foldImage(comm->algoFoldOrder[g], comm->foldAlgos[g]));
+    for (size_t g = 0; g < comm->algoFold.size(); g++)
+      if (!comm->algoFold[g].order.empty()) NCCLCHECK(foldImage(comm->algoFold[g], comm->foldAlgos[g]));
   }
   return ncclSuccess;
 }

@@ -111,3 +111,30 @@ def test_lowered_interpreted_and_flat_calls_interleave(tmp_path, monkeypatch):
             last, used = _case(cr, count, 6, it)
             kinds.add((k, last["small"] == 2, used))   # the interpreted call: general kernel (3 iterations)
         assert kinds == {(0, True, 0), (1, False, 0), (2, True, "ring")}, kinds
+
+
+RCCL = "/opt/rocm/share/rccl/msccl-algorithms"
+
+
+@pytest.mark.parametrize("nbytes", [512, 8192, 32768])
+def test_rccl_allpairs_lowered_with_chunk_classes(tmp_path, nbytes):
+    """RCCL's shipped msccl-tools all-pairs (8n LL 32 tb, fp16): its chunks fold in 7 orders
+    (each chunk's owner first), the fold kernel picks each pack's order by its chunk."""
+    p = os.path.join(RCCL, "allreduce-allpairs-8n-ll-32tb.xml")
+    if not os.path.exists(p):
+        pytest.skip("fixture missing")
+    with CoResident(8, [open(p).read()], str(tmp_path)) as cr:
+        for rep in range(2):
+            last, used = _case(cr, nbytes // 2, 6, rep + nbytes % 83)
+            assert last["small"] == 2 and last["algo"] == used == 0, last
+
+
+@pytest.mark.parametrize("n,count,dt,lowered", [(8, 2 * 64 * 8 * 8, 6, True), (4, 16 * 40, 7, True),
+                                                 (4, 16 * 41, 7, False)])
+def test_allpairs_classes_and_whole_packs(tmp_path, n, count, dt, lowered):
+    """The two-phase all-pairs: lowered when every chunk is whole 16-B packs (a pack folds in one
+    chunk's order); 41 floats per chunk are not, and the call keeps the interpreter."""
+    xml = xmlgen.allreduce_allpairs(n, 1, "LL", inplace=False)
+    with CoResident(n, [xml], str(tmp_path)) as cr:
+        last, _ = _case(cr, count, dt, count % 71, in_place=False)
+        assert (last["small"] == 2) == lowered, last

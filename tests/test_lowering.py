@@ -1,11 +1,12 @@
 """One-hop MSCCL AllReduce schedules run as the fold kernel (msccl_amd/csrc/lower.cc).
 
 The product decides symbolically, from every rank's program, whether a schedule's result is on
-every rank a left fold of all ranks' same chunk in one order per rank; this file pins that
-decision against the oracle: for every schedule the product lowers, oracle/sim.py (the reference's
-interpreter semantics, msccl_interpreter.h:66-205) running the XML gives bit for bit the fold in
-the product's order, on fp16 sums whose rounding depends on the order; schedules whose result is
-not such a fold are refused with the reason.  No GPU needed."""
+every rank, chunk by chunk, a left fold of all ranks' same chunk (chunks grouped into classes of
+equal orders); this file pins that decision against the oracle: for every schedule the product
+lowers, oracle/sim.py (the reference's interpreter semantics, msccl_interpreter.h:66-205) running
+the XML gives bit for bit, chunk by chunk, the fold in the product's order for that chunk's class,
+on fp16 sums whose rounding depends on the order; schedules whose result is not such a fold are
+refused with the reason.  No GPU needed."""
 import os
 
 import numpy as np
@@ -30,10 +31,13 @@ LOWERED = {
     "oneshot_unordered_3": (lambda: xmlgen.allreduce_oneshot(3, 1, "LL"), 3),
     "oneshot_ordered_16": (lambda: xmlgen.allreduce_oneshot(16, 1, "LL", ordered=True), 16),
     "allpairs_2": (lambda: xmlgen.allreduce_allpairs(2, 4, "LL"), 2),
+    # the two-phase all-pairs: each chunk's owner folds it first (one class per owner order)
+    "allpairs_8": (lambda: xmlgen.allreduce_allpairs(8, 1, "LL"), 8),
+    "allpairs_4_out_of_place": (lambda: xmlgen.allreduce_allpairs(4, 2, "LL", inplace=False), 4),
+    "rccl_allpairs_8n_ll_32tb": (lambda: open(os.path.join(RCCL, "allreduce-allpairs-8n-ll-32tb.xml")).read(), 8),
 }
 REFUSED = {
-    "allpairs_8": (lambda: xmlgen.allreduce_allpairs(8, 1, "LL"), 8, "differs between chunks"),
-    "ring_8": (lambda: xmlgen.allreduce_ring(8, 4, "LL"), 8, "differs between chunks"),
+    "ring_8": (lambda: xmlgen.allreduce_ring(8, 4, "LL"), 8, "more fold orders"),
     "pair_simple": (lambda: xmlgen.allreduce_pair_oneshot(1, "Simple"), 2, "not LL"),
     "oneshot_ll128": (lambda: xmlgen.allreduce_oneshot(4, 1, "LL128"), 4, "not LL"),
     "reduce_scatter": (lambda: xmlgen.reduce_scatter_allpairs(4, 1, "LL"), 4, "not a valid AllReduce"),
@@ -67,18 +71,25 @@ def _fold(ins, order, dt):
 @pytest.mark.parametrize("name", sorted(LOWERED))
 def test_lowered_schedules_equal_the_fold_in_their_order(tmp_path, name):
     gen, n = LOWERED[name]
-    xml = gen()
+    try:
+        xml = gen()
+    except OSError:
+        pytest.skip("fixture missing")
     info = M.lower_json(_path(tmp_path, name, xml), n)
     assert info["ok"] == 1, info
-    order = info["order"]
-    assert len(order) == n and all(sorted(o) == list(range(n)) for o in order)
+    classes, cls = info["classes"], info["chunkClass"]
+    assert all(len(k) == n and all(sorted(o) == list(range(n)) for o in k) for k in classes)
     a0 = L.parse_xml(xml, 0, n)
-    count = a0.nchunksperloop * 96      # fp16 sums of 96-element chunks: rounding depends on the order
+    assert len(cls) == a0.nchunksperloop and set(cls) == set(range(len(classes)))
+    per = 96                            # fp16 sums of 96-element chunks: rounding depends on the order
+    count = a0.nchunksperloop * per
     for dt, seed in ((6, 3), (9, 4), (7, 5)):
         ins, res = _oracle_run(xml, n, count, dt, bool(a0.inplace), seed)
         for r in range(n):
-            want = _fold(ins, order[r], dt)
-            assert np.array_equal(res[r].view(np.uint8), want.view(np.uint8)), (name, dt, r, order[r])
+            for c in range(a0.nchunksperloop):
+                sl = slice(c * per, (c + 1) * per)
+                want = _fold([x[sl] for x in ins], classes[cls[c]][r], dt)
+                assert np.array_equal(res[r][sl].view(np.uint8), want.view(np.uint8)), (name, dt, r, c)
 
 
 def test_order_is_sensitive():
@@ -93,12 +104,17 @@ def test_order_is_sensitive():
 
 def test_expected_orders(tmp_path):
     pair = M.lower_json(_path(tmp_path, "p", xmlgen.allreduce_pair_oneshot(2, "LL")), 2)
-    assert pair["order"] == [[0, 1], [0, 1]]
+    assert pair["classes"] == [[[0, 1], [0, 1]]] and pair["chunkClass"] == [0, 0]
     ordered = M.lower_json(_path(tmp_path, "o", xmlgen.allreduce_oneshot(8, 4, "LL", ordered=True)), 8)
-    assert ordered["order"] == [list(range(8))] * 8
+    assert ordered["classes"] == [[list(range(8))] * 8]
     unordered = M.lower_json(_path(tmp_path, "u", xmlgen.allreduce_oneshot(4, 1, "LL")), 4)
     # rank r: d = x_r first, then the peers ascending (fn(x_r, x_p0) is the innermost pair)
-    assert unordered["order"] == [[0, 1, 2, 3], [0, 1, 2, 3], [0, 2, 1, 3], [0, 3, 1, 2]]
+    assert unordered["classes"] == [[[0, 1, 2, 3], [0, 1, 2, 3], [0, 2, 1, 3], [0, 3, 1, 2]]]
+    # the two-phase all-pairs, 4 ranks: chunk j*4+m of an instance is owned by rank j, which folds
+    # it first; owners 0 and 1 give the same order (fn(x_0, x_1) either way): 3 classes
+    ap = M.lower_json(_path(tmp_path, "a", xmlgen.allreduce_allpairs(4, 1, "LL")), 4)
+    assert ap["chunkClass"] == [0] * 8 + [1] * 4 + [2] * 4
+    assert ap["classes"] == [[[0, 1, 2, 3]] * 4, [[0, 2, 1, 3]] * 4, [[0, 3, 1, 2]] * 4]
 
 
 @pytest.mark.parametrize("name", sorted(REFUSED))
@@ -108,14 +124,14 @@ def test_refused_schedules(tmp_path, name):
     assert info["ok"] == 0 and why in info["why"], info
 
 
-def test_rccl_shipped_allpairs_is_refused():
+def test_rccl_shipped_allpairs_lowers_with_one_class_per_owner_order():
     """msccl-tools' two-phase all-pairs (RCCL's 8n 32-tb file): the owner of each chunk folds it
-    first, so the order differs between chunks; it keeps the interpreter."""
+    first, so chunks fall into 7 classes (owners 0 and 1 fold alike)."""
     p = os.path.join(RCCL, "allreduce-allpairs-8n-ll-32tb.xml")
     if not os.path.exists(p):
         pytest.skip("fixture missing")
     info = M.lower_json(p, 8)
-    assert info["ok"] == 0 and "differs between chunks" in info["why"], info
+    assert info["ok"] == 1 and len(info["classes"]) == 7 and len(info["chunkClass"]) == 256, info
 
 
 def test_broken_schedule_is_refused(tmp_path):

@@ -13,6 +13,8 @@
 #   xover     the lowered fold against the interpreter, 8 KiB - 128 KiB (MSCCL_AMD_LOWER_MAX_BYTES)
 #   c4trace   where the 8-rank C4 ring launch waits (tools/trace_report.py --summary)
 #   xcdpmc    rocprofv3's counter list and per-instance TCC request counters of the C2 launch
+#   prof      tools/profile.sh on the C2 headline (kernel stats, FETCH_SIZE, WRITE_SIZE)
+#   prof8     the same on the 8-rank C3 shape and C4 / C5 (per-kernel traffic)
 # e.g. STEPS="suite lat" LIBS="tools/ab/a.so msccl_amd/libmsccl_amd.so" TAG=r04a bash tools/gpu_session.sh
 set -o pipefail
 export TMPDIR=/tmp
@@ -30,12 +32,16 @@ for step in $STEPS; do
       > ${O}_suite.txt 2>&1 || fail suite ${O}_suite.txt
     tail -2 ${O}_suite.txt ;;
   lat)
+    # LATSPECS: "schedule bytes ranks instances dtype" entries separated by ';'; LATENV: extra
+    # environment for every run (e.g. MSCCL_AMD_LOWER=0)
+    SPECS=${LATSPECS:-"pair 128 2 1 7;pair 4096 2 16 7;pair 65536 2 16 7;oneshot 128 8 4 6;oneshot 4096 8 4 6;fbtree 128 2 1 7;fbtree 128 8 1 6"}
     for L in $LIBS; do
-      for spec in "pair 128 2 1 7" "pair 4096 2 16 7" "pair 65536 2 16 7" "oneshot 128 8 4 6" "oneshot 4096 8 4 6" \
-                  "fbtree 128 2 1 7" "fbtree 128 8 1 6"; do
+      IFS=';' read -ra SP <<< "$SPECS"
+      for spec in "${SP[@]}"; do
         set -- $spec
-        r=$(MSCCL_AMD_LIB=$L lat --schedule $1 --bytes $2 --ranks $3 --instances $4 --dtype $5) || fail "lat $L $spec"
-        echo "$(basename $L) $r" | tee -a ${O}_lat.txt
+        r=$(env $LATENV MSCCL_AMD_LIB=$L timeout -k 5 90 python3 tools/lat_one.py --iters 300 --graph --schedule $1 \
+            --bytes $2 --ranks $3 --instances $4 --dtype $5 2>&1 | grep -v amdgpu.ids) || fail "lat $L $spec"
+        echo "$(basename $L) $LATENV $r" | tee -a ${O}_lat.txt
       done
     done ;;
   xover)
@@ -59,7 +65,7 @@ for step in $STEPS; do
     timeout -s KILL 60 rocprofv3 -L > ${O}_counters.txt 2>&1 || fail "rocprofv3 -L" ${O}_counters.txt
     for c in TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_HIT TCC_MISS; do
       timeout -s KILL 120 rocprofv3 --pmc $c --output-format json csv -d gpurun_out/${TAG}_xcd_$c -o run -- \
-        python3 bench.py --sizes 33554432 --steps 10 --warmup 3 --no-cpu --quiet --no-secondary --pmc off --extras "" \
+        python3 bench.py --sizes 33554432 --steps 10 --warmup 3 --no-cpu --quiet --no-secondary --pmc off --extras "" --eager \
         > /dev/null 2> ${O}_xcd_$c.err || fail "xcdpmc $c" ${O}_xcd_$c.err
       # keep a summary and the head of the JSON (its per-dimension layout), not the raw output
       d=gpurun_out/${TAG}_xcd_$c
@@ -68,6 +74,16 @@ for step in $STEPS; do
       } > ${O}_xcd_$c.txt 2>&1
       rm -rf $d
     done ;;
+  prof)
+    # rocprofv3 kernel trace + stats and the FETCH_SIZE / WRITE_SIZE passes of the C2 headline
+    # (tools/profile.sh -> gpurun_out/prof_${TAG}_final/, profiles/ files copied there)
+    bash tools/profile.sh ${TAG}_final > ${O}_prof.txt 2>&1 || fail prof ${O}_prof.txt
+    tail -c 600 ${O}_prof.txt ;;
+  prof8)
+    # the same passes over the 8-rank C3 shape (32 MiB) and the C4 / C5 configs: per-kernel traffic
+    bash tools/profile.sh ${TAG}_extras8 --vranks 8 --dtype fp16 --sizes 33554432 --extras C4,C5 --no-cpu --quiet \
+      --pmc off --no-secondary --steps 5 --warmup 2 > ${O}_prof8.txt 2>&1 || fail prof8 ${O}_prof8.txt
+    tail -c 600 ${O}_prof8.txt ;;
   trace)
     MSCCL_AMD_LIB=${LATLIB:-tools/ab/libmsccl_amd_lat.so} MSCCL_AMD_TRACE=2 timeout -k 5 90 python3 tools/lat_trace.py \
       > ${O}_trace.txt 2>&1 || fail trace ${O}_trace.txt

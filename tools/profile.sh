@@ -10,6 +10,8 @@ shift
 # --pmc off: under rocprofv3 the bench must not start its own profiler child (an exec from a process
 # the outer profiler has initialised); --no-secondary: every interpreter dispatch is a headline launch
 ARGS=${@:-"--no-cpu --quiet --sizes 33554432 --steps 20 --warmup 5 --pmc off --no-secondary"}
+# counters per dispatch: eager launches (one dispatch per step, no graph in the profiled process)
+ARGS="$ARGS --eager"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
