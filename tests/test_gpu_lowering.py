@@ -138,3 +138,14 @@ def test_allpairs_classes_and_whole_packs(tmp_path, n, count, dt, lowered):
     with CoResident(n, [xml], str(tmp_path)) as cr:
         last, _ = _case(cr, count, dt, count % 71, in_place=False)
         assert (last["small"] == 2) == lowered, last
+
+
+@pytest.mark.parametrize("inst", [1, 2])
+def test_ring_lowered_per_start_class(tmp_path, inst):
+    """An 8-rank LL ring of 1 or 2 rings: each chunk folds along its ring from the rank after its
+    owner (8 / 16 classes); the fold kernel gives the ring's bits at small sizes."""
+    xml = xmlgen.allreduce_ring(8, inst, "LL")
+    with CoResident(8, [xml], str(tmp_path)) as cr:
+        for count, dt in ((8 * inst * 64, 6), (8 * inst * 8 * 37, 9)):
+            last, _ = _case(cr, count, dt, count % 53)
+            assert last["small"] == 2, last

@@ -34,10 +34,13 @@ LOWERED = {
     # the two-phase all-pairs: each chunk's owner folds it first (one class per owner order)
     "allpairs_8": (lambda: xmlgen.allreduce_allpairs(8, 1, "LL"), 8),
     "allpairs_4_out_of_place": (lambda: xmlgen.allreduce_allpairs(4, 2, "LL", inplace=False), 4),
+    # rings: one class per (ring, start rank) of the reduce-scatter leg
+    "ring_8x1": (lambda: xmlgen.allreduce_ring(8, 1, "LL"), 8),
+    "ring_8x2": (lambda: xmlgen.allreduce_ring(8, 2, "LL"), 8),
     "rccl_allpairs_8n_ll_32tb": (lambda: open(os.path.join(RCCL, "allreduce-allpairs-8n-ll-32tb.xml")).read(), 8),
 }
 REFUSED = {
-    "ring_8": (lambda: xmlgen.allreduce_ring(8, 4, "LL"), 8, "more fold orders"),
+    "ring_8x4": (lambda: xmlgen.allreduce_ring(8, 4, "LL"), 8, "more fold orders"),   # 32 orders
     "pair_simple": (lambda: xmlgen.allreduce_pair_oneshot(1, "Simple"), 2, "not LL"),
     "oneshot_ll128": (lambda: xmlgen.allreduce_oneshot(4, 1, "LL128"), 4, "not LL"),
     "reduce_scatter": (lambda: xmlgen.reduce_scatter_allpairs(4, 1, "LL"), 4, "not a valid AllReduce"),
