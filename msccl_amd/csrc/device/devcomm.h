@@ -184,7 +184,7 @@ struct RankWork {
   uint64_t* flags;
   uint64_t* epochs;
   int32_t maxSplit;
-  int32_t pad0;
+  int32_t foldPacksPerWg;       // fold kernel: packs per workgroup, floor(packs / split) (no division on the device)
   const char* images;           // thread-block images, tbStride bytes each
   int32_t tbStride;
   int32_t connSplit;            // connection record of (tb, sub): send / recv [tb * connSplit + sub]

@@ -1378,41 +1378,53 @@ struct Interp {
     nkBuf = nullptr;
     scG = nullptr;
     rcG = nullptr;
+    // every kernel argument the prologue's loads need, in one batch (pinArgs)
     const int np = w.foldPeers;
+    const int n = (int)w.sizePerChunk;
+    const int split = w.split, base = w.foldPacksPerWg, connSplit = w.connSplit, tbStride = w.tbStride;
+    const int mode = w.ringColl;
+    const char* const images = w.images;
+    DevSendConn* const sendG = w.send;
+    DevRecvConn* const recvG = w.recv;
+    uint64_t* const epochs = w.epochs;
+    const void* const sendbuff = w.sendbuff;
+    void* const recvbuff = w.recvbuff;
+    pinArgs(np, n, split, base, connSplit, tbStride, mode, images, sendG, recvG, epochs, sendbuff, recvbuff);
     constexpr int E = 8 / TS;
     constexpr int G = 8;  // peers per wait
-    const int n = (int)w.sizePerChunk;
     const int npkAll = (n + PE - 1) / PE;
-    // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges,
-    // cut into FIFO steps on its own sub-connection of every peer
-    const int p0 = (int)((int64_t)npkAll * wg / w.split);
-    const int npk = (int)((int64_t)npkAll * (wg + 1) / w.split) - p0;
+    // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges (the
+    // first npkAll % split ranges one pack longer), cut into FIFO steps on its own sub-connection
+    // of every peer.  The host's quotient: a 64-bit division here ran ahead of the first load
+    const int rem = npkAll - base * split;
+    const int p0 = wg * base + min(wg, rem);
+    const int npk = base + (wg < rem ? 1 : 0);
     const int nlinesFull = (n + E - 1) / E;
-    const __amdgpu_buffer_rsrc_t srs = makeRsrc(w.sendbuff), drs = makeRsrc(w.recvbuff);
-    const bool vec = aligned16(w.sendbuff) && aligned16(w.recvbuff);
+    const __amdgpu_buffer_rsrc_t srs = makeRsrc(sendbuff), drs = makeRsrc(recvbuff);
+    const bool vec = aligned16(sendbuff) && aligned16(recvbuff);
     // one round trip: thread block 0's image (the fold order), every peer's send and recv
     // records, the launch epoch, and this lane's first input pack (step 0, q = tid: the pack
     // p0 + tid in every FIFO cut; the ReduceScatter reads the blocks the image names instead),
     // so the input's load does not wait for the image's
     u32x4 pre = {0, 0, 0, 0};
-    const bool havePre = w.ringColl != kRingReduceScatter && tid < npk;
+    const bool havePre = mode != kRingReduceScatter && tid < npk;
     {
       // issued first: the lane's later waits (for its image unit or record) then cover it too
       if (havePre) pre = loadPack(srs, vec, p0 + tid, n);
-      const u32x4* gimg = (const u32x4*)w.images;
-      const int nU = w.tbStride >> 4;
+      const u32x4* gimg = (const u32x4*)images;
+      const int nU = tbStride >> 4;
       for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
       if (tid >= 64 && tid < 64 + 4 * np) {
         const int k = (tid - 64) >> 2, j = (tid - 64) & 3;
-        ((u32x4*)&fs->foldSend[k])[j] = ((const u32x4*)(w.send + (size_t)(k + 1) * w.connSplit + wg))[j];
+        ((u32x4*)&fs->foldSend[k])[j] = ((const u32x4*)(sendG + (size_t)(k + 1) * connSplit + wg))[j];
       }
       if (tid >= 192 && tid < 192 + 4 * np) {
         const int k = (tid - 192) >> 2, j = (tid - 192) & 3;
-        ((u32x4*)&fs->foldRecv[k])[j] = ((const u32x4*)(w.recv + (size_t)(k + 1) * w.connSplit + wg))[j];
+        ((u32x4*)&fs->foldRecv[k])[j] = ((const u32x4*)(recvG + (size_t)(k + 1) * connSplit + wg))[j];
       }
       if (tid == 128) {
         sh->aborted = 0;
-        sh->epoch = atomicLoadAgent(w.epochs + wg);  // slot wg of the fold's range
+        sh->epoch = atomicLoadAgent(epochs + wg);  // slot wg of the fold's range
       }
     }
     __syncthreads();
@@ -1445,7 +1457,6 @@ struct Interp {
     // the collective (RankWork::ringColl): 0 the AllReduce (the flat tree), kRingReduceScatter,
     // kRingAllGather; the image's transfers 0 / 1 carry the AllReduce / ReduceScatter fold orders
     // and transfer 2 the rank of every peer record (then this rank) (transport.cc: ringUpload)
-    const int mode = w.ringColl;
     const DevTransfer* tr0 = (const DevTransfer*)&sh->img[1];
     const int16_t* reds = (const int16_t*)(tr0 + hd.nsteps) + 2 * hd.ndeps;
     const DevTransfer t = loadTransfer(tr0 + (mode == kRingReduceScatter ? 1 : 0));
@@ -1809,12 +1820,39 @@ __device__ __forceinline__ int rankOfBlock(const LaunchArgsN<R>& args, int b) {
   return r;
 }
 
+// Kernel arguments into the scalar cache in one round trip: one load per 64-B line of [p, p +
+// BYTES), all issued before the first is used (pinArgs).  The kernel-argument fields a prologue
+// reads are spread over a RankWork's four lines, and the compiler issues them in several batches,
+// each waiting for the last: every batch that touched a new line paid a cache miss.
+template <int BYTES>
+__device__ __forceinline__ void warmArgLines(const void* p) {
+  const char* c = (const char*)p;
+  uint32_t v[(BYTES + 63) / 64];
+#pragma unroll
+  for (int i = 0; i < (BYTES + 63) / 64; i++) v[i] = *(const uint32_t*)(c + (i * 64 < BYTES - 4 ? i * 64 : BYTES - 4));
+#pragma unroll
+  for (int i = 0; i < (BYTES + 63) / 64; i++) pinArg(v[i]);
+}
+
+// The RankWork of block b: the whole argument block warmed first when it is the compact one (R <=
+// kCompactLaunchRanks, 424 B), else the rank's own RankWork after the lookup.
+template <int R>
+__device__ __forceinline__ const RankWork& rankWorkOf(const LaunchArgsN<R>& args, int b) {
+#ifndef MSCCL_EXP_NOWARM
+  if constexpr (R <= kCompactLaunchRanks) warmArgLines<sizeof(LaunchArgsN<R>)>(&args);
+#endif
+  const RankWork& w = args.w[rankOfBlock(args, b)];
+#ifndef MSCCL_EXP_NOWARM
+  if constexpr (R > kCompactLaunchRanks) warmArgLines<sizeof(RankWork)>(&w);
+#endif
+  return w;
+}
+
 template <typename T, int OP, int PROTO>
 __global__ void __launch_bounds__(kNT, 4) mscclKernel(const LaunchArgs args) {
   __shared__ BlockShared sh;
   const int b = blockIdx.x;
-  const int r = rankOfBlock(args, b);
-  const RankWork& w = args.w[r];
+  const RankWork& w = rankWorkOf(args, b);
   const int local = b - w.blockBase;
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
@@ -1827,8 +1865,7 @@ template <typename T, int OP, int PROTO, int R, int SET>
 __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> args) {
   __shared__ BlockShared sh;
   const int b = blockIdx.x;
-  const int r = rankOfBlock(args, b);
-  const RankWork& w = args.w[r];
+  const RankWork& w = rankWorkOf(args, b);
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
   it.template runSmall<SET>(w, b - w.blockBase);
@@ -1841,10 +1878,10 @@ __global__ void __launch_bounds__(kNT, 1) mscclFoldKernel(const LaunchArgsN<R> a
   __shared__ BlockShared sh;
   __shared__ FoldShared fs;
   const int b = blockIdx.x;
-  const int r = rankOfBlock(args, b);
+  const RankWork& w = rankWorkOf(args, b);
   Interp<T, OP, pLL> it;
   it.sh = &sh;
-  it.runFold(args.w[r], b - args.w[r].blockBase, &fs);
+  it.runFold(w, b - w.blockBase, &fs);
 }
 
 }  // namespace msccl

@@ -50,6 +50,19 @@ __device__ __forceinline__ uint64_t uni(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Kernel-argument values a prologue needs, held in SGPRs from here on: without it the compiler
+// sinks each scalar load into the branch that uses it, and every lane group's load chain starts
+// with its own kernel-argument round trip (three in a row in the fold kernel).  An empty asm
+// statement with SGPR inputs: no instruction, only the order of issue.
+template <class A>
+__device__ __forceinline__ void pinArg(const A& a) {
+  asm volatile("" ::"s"(a));
+}
+template <class... A>
+__device__ __forceinline__ void pinArgs(const A&... a) {
+  (pinArg(a), ...);
+}
+
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
 template <int AUX>
 __device__ __forceinline__ u32x3 ld12(__amdgpu_buffer_rsrc_t r, uint32_t off) {

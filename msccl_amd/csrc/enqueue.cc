@@ -229,6 +229,7 @@ RankWork makeFlatWork(Planned& p) {
   const int64_t npk = (p.plan.sizePerChunk + pe - 1) / pe;
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(kFlatSubs, (npk + kFoldPacksPerWg - 1) / kFoldPacksPerWg));
   w.split = (uint8_t)wgs;
+  w.foldPacksPerWg = (int32_t)(npk / wgs);
   w.maxOpElems = (int64_t)kMaxRunSlots * (comm->llSlotLines / 2) * pe;
   int merge = 1;
   if (p.plan.nIters > 1 && p.plan.maxAllowedCount == 1) {  // makeWork's rule, send runs of one chunk

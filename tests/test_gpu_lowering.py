@@ -116,17 +116,18 @@ def test_lowered_interpreted_and_flat_calls_interleave(tmp_path, monkeypatch):
 RCCL = "/opt/rocm/share/rccl/msccl-algorithms"
 
 
-@pytest.mark.parametrize("nbytes", [512, 8192, 32768])
+@pytest.mark.parametrize("nbytes", [512, 4096, 8192, 32768])
 def test_rccl_allpairs_lowered_with_chunk_classes(tmp_path, nbytes):
-    """RCCL's shipped msccl-tools all-pairs (8n LL 32 tb, fp16): its chunks fold in 7 orders
-    (each chunk's owner first), the fold kernel picks each pack's order by its chunk."""
+    """RCCL's shipped msccl-tools all-pairs (8n LL 32 tb, fp16): its 256 chunks fold in 7 orders
+    (each chunk's owner first), the fold kernel picks each pack's order by its chunk.  512 B is
+    one element per chunk, not whole 16-B packs: that call keeps the interpreter."""
     p = os.path.join(RCCL, "allreduce-allpairs-8n-ll-32tb.xml")
     if not os.path.exists(p):
         pytest.skip("fixture missing")
     with CoResident(8, [open(p).read()], str(tmp_path)) as cr:
         for rep in range(2):
             last, used = _case(cr, nbytes // 2, 6, rep + nbytes % 83)
-            assert last["small"] == 2 and last["algo"] == used == 0, last
+            assert (last["small"] == 2) == (nbytes >= 4096) and last["algo"] == used == 0, last
 
 
 @pytest.mark.parametrize("n,count,dt,lowered", [(8, 2 * 64 * 8 * 8, 6, True), (4, 16 * 40, 7, True),
