@@ -1834,17 +1834,13 @@ __device__ __forceinline__ void warmArgLines(const void* p) {
   for (int i = 0; i < (BYTES + 63) / 64; i++) pinArg(v[i]);
 }
 
-// The RankWork of block b: the whole argument block warmed first when it is the compact one (R <=
-// kCompactLaunchRanks, 424 B), else the rank's own RankWork after the lookup.
+// The RankWork of block b, its lines warmed after the lookup in the launches of more than
+// kCompactLaunchRanks ranks (8 ranks: 0.2-0.35 us less per launch).  The compact launches do
+// without: warming their whole 424-B block first cost 0.2-0.5 us (profiles/r04f_lat.txt).
 template <int R>
 __device__ __forceinline__ const RankWork& rankWorkOf(const LaunchArgsN<R>& args, int b) {
-#ifndef MSCCL_EXP_NOWARM
-  if constexpr (R <= kCompactLaunchRanks) warmArgLines<sizeof(LaunchArgsN<R>)>(&args);
-#endif
   const RankWork& w = args.w[rankOfBlock(args, b)];
-#ifndef MSCCL_EXP_NOWARM
   if constexpr (R > kCompactLaunchRanks) warmArgLines<sizeof(RankWork)>(&w);
-#endif
   return w;
 }
 

@@ -270,7 +270,8 @@ def test_hip_graph_capture_and_replay(proto, sched, tmp_path):
 
 def test_device_trace_records_every_transfer(tmp_path, monkeypatch):
     """MSCCL_AMD_TRACE=1: every workgroup of the last launch leaves a header, a setup event, a
-    begin/end pair per executed transfer and an end event, in time order."""
+    begin/end pair per executed transfer and an end event, in time order.  (The interpreter's
+    trace: the 2-rank all-pairs is lowered to the fold kernel otherwise, which traces one pass.)"""
     import torch
     import msccl_amd as M
     from msccl_amd import xmlgen
@@ -278,6 +279,7 @@ def test_device_trace_records_every_transfer(tmp_path, monkeypatch):
     xml.write_text(xmlgen.allreduce_allpairs(2, 1, "LL"))
     monkeypatch.setenv("MSCCL_XML_FILES", str(xml))
     monkeypatch.setenv("MSCCL_AMD_TRACE", "1")
+    monkeypatch.setenv("MSCCL_AMD_LOWER", "0")
     comms = M.Comm.init_all([0, 0])
     try:
         bufs = [torch.ones(4 * 256, device="cuda") for _ in comms]
