@@ -36,7 +36,9 @@ def test_two_ops_per_comm_in_a_group(tmp_path, monkeypatch, ref):
         torch.cuda.synchronize()
         assert all(c.async_error() == 0 for c in cr.comms)
         last = [c.info()["last"] for c in cr.comms]
-        assert all((l["ringColl"] != 0) == (ref == "1") for l in last), last
+        # the fallback (algo -1) only under the reference's selection; the schedule (algo 0) runs
+        # interpreted or lowered to the fold kernel otherwise
+        assert all((l["algo"] < 0) == (ref == "1") for l in last), last
         for ins, t in ((xa, ta), (xb, tb)):
             if ref == "1":
                 want, _ = R.run(L.ALLREDUCE, count, dt, 0, [x.copy() for x in ins], [None] * n, True)

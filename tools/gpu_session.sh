@@ -28,7 +28,7 @@ lat() { timeout -k 5 90 python3 tools/lat_one.py --iters 300 --graph "$@" 2>&1 |
 for step in $STEPS; do
   case $step in
   suite)
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider \
+    timeout -k 10 900 python -u -m pytest tests -m gpu ${SUITEARGS:--x} -q --timeout 120 --timeout-method thread -p no:cacheprovider \
       > ${O}_suite.txt 2>&1 || fail suite ${O}_suite.txt
     tail -2 ${O}_suite.txt ;;
   lat)
