@@ -12,6 +12,7 @@
 #   sweep     bench.py sweeps of every library in LIBS (C2 2 ranks, then C3 shape 8 ranks fp16)
 #   xover     the lowered fold against the interpreter, 8 KiB - 128 KiB (MSCCL_AMD_LOWER_MAX_BYTES)
 #   c4trace   where the 8-rank C4 ring launch waits (tools/trace_report.py --summary)
+#   c4knobs   the 8-rank C4 shape under each environment of C4ENVS (';'-separated)
 #   xcdpmc    rocprofv3's counter list and per-instance TCC request counters of the C2 launch
 #   prof      tools/profile.sh on the C2 headline (kernel stats, FETCH_SIZE, WRITE_SIZE)
 #   prof8     the same on the 8-rank C3 shape and C4 / C5 (per-kernel traffic)
@@ -59,6 +60,15 @@ for step in $STEPS; do
     MSCCL_AMD_TRACE=1 timeout -k 10 300 python3 tools/trace_report.py --schedule ring --ranks 8 --instances 32 --proto Simple \
       --dtype 9 --bytes 268435456 --iters 3 --summary > ${O}_c4trace.txt 2>&1 || fail c4trace ${O}_c4trace.txt
     cat ${O}_c4trace.txt ;;
+  c4knobs)
+    IFS=';' read -ra EV <<< "${C4ENVS:-NCCL_BUFFSIZE=4194304}"
+    for e in "${EV[@]}"; do
+      env $e timeout -k 10 300 python3 bench.py --vranks 8 --dtype fp16 --sizes 128 --extras C4 --no-cpu --pmc off \
+        --no-secondary --steps 5 --warmup 2 > ${O}_c4k.json 2>> ${O}_c4k.err || fail "c4knobs $e" ${O}_c4k.err
+      python3 -c "
+import json; d = json.load(open('${O}_c4k.json'))['configs']['C4']
+print('$e', d['allreduce']['kernel_ms'], d['allreduce']['hbm_frac'], d['verified'])" | tee -a ${O}_c4knobs.txt
+    done ;;
   xcdpmc)
     # per-XCD memory requests of the C2 headline launch: the counters' dimensions, then one pass
     # with the per-instance output kept (JSON)
