@@ -419,6 +419,7 @@ struct Interp {
     sendStep++;
   }
 
+  template <bool REPOLL>
   __device__ void llFusedOp(const T* src, T* dst, const Shape s) {
     const int slotLines = uni(sc->llSlotLines);
     const int slotPacks = slotLines / 2;
@@ -465,10 +466,12 @@ struct Interp {
         la[2 * u + 1] = two[u] ? rslot + llLineIdx(q, 1) : la[2 * u];
       }
       ldLines8(la, ln);
-#ifdef MSCCL_EXP_BALLOT
-      // measurement build ("LL polls"): a wave-wide spin, every lane re-polling all
-      // its lines until no lane of the wave sees a stale flag
-      {
+      // REPOLL (the exchange-set kernel, DESIGN.md §2 "LL polls"): every line of the lane
+      // re-polled together while any is stale (one round trip for the late lines, not one per
+      // pair); the per-pair loop below then finds every flag current.  32 MiB: 63.4 us against
+      // 64.6 for per-pair polls, a wave-ballot spin 63.5 (profiles/r04i_lat.txt).  The general
+      // small kernel keeps the per-pair polls: the loop's live lines spill its fp16 form
+      if constexpr (REPOLL) {
         Spin spins;
         while (true) {
           bool stale = false;
@@ -476,12 +479,10 @@ struct Interp {
           for (int u = 0; u < U; u++)
             stale |= act[u] && (ln[2 * u].y != rflag || ln[2 * u].w != rflag || ln[2 * u + 1].y != rflag ||
                                 ln[2 * u + 1].w != rflag);
-          if (__builtin_amdgcn_ballot_w64(stale) == 0) break;
-          if (spinAbort(spins)) break;
+          if (!stale || spinAbort(spins)) break;
           ldLines8(la, ln);
         }
       }
-#endif
 #pragma unroll
       for (int u = 0; u < U; u++) {
         Spin spins;
@@ -1084,7 +1085,7 @@ struct Interp {
         case tSend: op<0, 1, 1, 0>(srcP + srcoff, nullptr, s); __syncthreads(); break;
         case tRRC: op<1, 0, 1, 1>(srcP + srcoff, dstP + dstoff, s); break;
         case tSendRrc:
-          if constexpr (FUSE && PROTO == pLL && OP <= 3) [[clang::always_inline]] llFusedOp(srcP + srcoff, dstP + dstoff, s);
+          if constexpr (FUSE && PROTO == pLL && OP <= 3) [[clang::always_inline]] llFusedOp<true>(srcP + srcoff, dstP + dstoff, s);
           break;
         default: return false;
       }
@@ -1102,7 +1103,7 @@ struct Interp {
       case tSendRrc:  // LL only (run / runSmall turn it into tSend otherwise); dst from the rrc
         if constexpr (FUSE && PROTO == pLL && OP <= 3) {  // MSCCL schedules run Sum..Min only
           // inlined like the other primitive calls (a call frame costs scratch and SGPR spills)
-          [[clang::always_inline]] llFusedOp(srcP + srcoff, dstP + dstoff, s);
+          [[clang::always_inline]] llFusedOp<false>(srcP + srcoff, dstP + dstoff, s);
         }
         break;
       case tRe: reduce(srcP, red + t.redPtr, reOff, sizePer, t.numReds, dstP + dstoff, s); __syncthreads(); break;

@@ -203,6 +203,9 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     for (auto& q : recs) c += !strcmp(r.host, q.host) && !strcmp(r.bus, q.bus);
     maxCo = std::max(maxCo, c);
   }
+  // every rank on one GPU: the local Simple FIFO size (plan.h: kLocalSimpleBuff), the same
+  // decision on every rank (the same records)
+  if (maxCo == (int)recs.size() && !comm->knobs.simpleBuffEnv) comm->knobs.buffSizes[kProtoSimple] = kLocalSimpleBuff;
   const SplitRecord& mine = recs[comm->rank];
   comm->coResident = 0;
   for (auto& q : recs) comm->coResident += !strcmp(mine.host, q.host) && !strcmp(mine.bus, q.bus);

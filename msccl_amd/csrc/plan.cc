@@ -69,6 +69,7 @@ Knobs Knobs::fromEnv() {
   k.buffSizes[kProtoLL] = envInt("NCCL_LL_BUFFSIZE", 8 * 512 * kFifoSteps * 16);
   k.buffSizes[kProtoLL128] = envInt("NCCL_LL128_BUFFSIZE", 120 * 640 * kFifoSteps * 8);
   k.buffSizes[kProtoSimple] = envInt("NCCL_BUFFSIZE", 1 << 22);
+  k.simpleBuffEnv = getenv("NCCL_BUFFSIZE") != nullptr;
   k.ringChannels = (int32_t)envInt("MSCCL_AMD_RING_CHANNELS", 0);
   k.split = (int32_t)envInt("MSCCL_AMD_SPLIT", 0);
   k.targetWgs = (int32_t)envInt("MSCCL_AMD_TARGET_WGS", 512);

@@ -78,10 +78,17 @@ struct Knobs {
   int32_t fuse;              // MSCCL_AMD_FUSE: fused s + rrc exchanges (transport.cc: fusableTbs)
   int32_t treeFlat;          // MSCCL_AMD_TREE_FLAT: the tree's values in one hop (plan.cc: makeFlatTreePlan)
   int32_t lower;             // MSCCL_AMD_LOWER: one-hop AllReduce schedules run as the fold (lower.cc)
-  int32_t pad0;
+  int32_t simpleBuffEnv;     // NCCL_BUFFSIZE was set (else a communicator of one GPU takes kLocalSimpleBuff)
   int64_t lowerMaxBytes;     // MSCCL_AMD_LOWER_MAX_BYTES: largest call (bytes per rank) lowered (-1: by ranks)
   static Knobs fromEnv();
 };
+
+// The Simple FIFO of a communicator whose ranks all share one GPU, unless NCCL_BUFFSIZE is set:
+// 256 KiB (eight 32-KiB slots) instead of the reference's 4 MiB.  Every FIFO hand-off then stays
+// in the L2 / MALL, and a ring's per-step skew costs 32-KiB steps: the 8-rank C4 ring 2.07 ->
+// 1.47 ms, C5 and the 2-rank shapes 3-25 % faster (profiles/r04i_c4knobs.txt, r04j_c4knobs.txt;
+// 128 and 64 KiB lose again).  Connections between GPUs keep the reference's size.
+constexpr int64_t kLocalSimpleBuff = 256 << 10;
 
 int refTypeSize(int dtype);
 bool inPlaceOf(int coll, const void* send, const void* recv, size_t count, int dtype, int rank);

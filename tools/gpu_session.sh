@@ -63,11 +63,13 @@ for step in $STEPS; do
   c4knobs)
     IFS=';' read -ra EV <<< "${C4ENVS:-NCCL_BUFFSIZE=4194304}"
     for e in "${EV[@]}"; do
-      env $e timeout -k 10 300 python3 bench.py --vranks 8 --dtype fp16 --sizes 128 --extras C4 --no-cpu --pmc off \
-        --no-secondary --steps 5 --warmup 2 > ${O}_c4k.json 2>> ${O}_c4k.err || fail "c4knobs $e" ${O}_c4k.err
+      env $e timeout -k 10 300 python3 bench.py --vranks ${C4RANKS:-8} --dtype fp16 --sizes 128 --extras ${C4CFG:-C4} --no-cpu \
+        --pmc off --no-secondary --steps 5 --warmup 2 > ${O}_c4k.json 2>> ${O}_c4k.err || fail "c4knobs $e" ${O}_c4k.err
       python3 -c "
-import json; d = json.load(open('${O}_c4k.json'))['configs']['C4']
-print('$e', d['allreduce']['kernel_ms'], d['allreduce']['hbm_frac'], d['verified'])" | tee -a ${O}_c4knobs.txt
+import json
+for c, d in json.load(open('${O}_c4k.json'))['configs'].items():
+    print('${C4RANKS:-8} ranks', c, '$e', ' '.join('%s %s ms %s' % (k, v['kernel_ms'], v['hbm_frac']) for k, v in d.items()
+          if isinstance(v, dict) and 'kernel_ms' in v), d.get('verified'), d.get('error', ''))" | tee -a ${O}_c4knobs.txt
     done ;;
   xcdpmc)
     # per-XCD memory requests of the C2 headline launch: the counters' dimensions, then one pass
