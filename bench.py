@@ -40,8 +40,8 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs, one rank each (default 1: config C2 with 2 ranks co-resident on cuda:0). "
                          "Without torch.distributed.run's WORLD_SIZE, N > 1 starts N rank processes itself")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=100, help="timed steps per size (one hipGraph of K launches; 100 keeps the graph launch under 0.2 us per step)")
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--vranks", type=int, default=2, help="co-resident ranks at --gpus 1 (config C2: 2)")
     ap.add_argument("--proto", default="LL")
     ap.add_argument("--dtype", default=None)
