@@ -203,9 +203,6 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     for (auto& q : recs) c += !strcmp(r.host, q.host) && !strcmp(r.bus, q.bus);
     maxCo = std::max(maxCo, c);
   }
-  // every rank on one GPU: the local Simple FIFO size (plan.h: kLocalSimpleBuff), the same
-  // decision on every rank (the same records)
-  if (maxCo == (int)recs.size() && !comm->knobs.simpleBuffEnv) comm->knobs.buffSizes[kProtoSimple] = kLocalSimpleBuff;
   const SplitRecord& mine = recs[comm->rank];
   comm->coResident = 0;
   for (auto& q : recs) comm->coResident += !strcmp(mine.host, q.host) && !strcmp(mine.bus, q.bus);
@@ -223,6 +220,15 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
   }
+  // every rank on one GPU: the local Simple FIFO size (plan.h: kLocalSimpleBuff), the same
+  // decision on every rank (the same records).  Only when every Simple schedule sends at most
+  // two chunks before it receives: a call moves up to chunkSize = half the FIFO per chunk, and a
+  // longer run of sends must fit the FIFO whole while its peer sends too (RCCL's 8-rank Simple
+  // all-pairs sends 8 chunks first: it keeps the reference's size)
+  bool smallFifo = maxCo == (int)recs.size() && !comm->knobs.simpleBuffEnv;
+  for (size_t a = 0; a < comm->algos.size(); a++)
+    if (comm->algos[a].proto == kProtoSimple && comm->algoSendRun[a] > 2) smallFifo = false;
+  if (smallFifo) comm->knobs.buffSizes[kProtoSimple] = kLocalSimpleBuff;
   // a schedule runs as the fold only when every rank found it one (the two ends of every flat
   // connection must run the same kernel)
   for (size_t a = 0; a < comm->algoFold.size() && a < (size_t)kMaxAlgos; a++)

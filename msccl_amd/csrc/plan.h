@@ -87,7 +87,9 @@ struct Knobs {
 // 256 KiB (eight 32-KiB slots) instead of the reference's 4 MiB.  Every FIFO hand-off then stays
 // in the L2 / MALL, and a ring's per-step skew costs 32-KiB steps: the 8-rank C4 ring 2.07 ->
 // 1.47 ms, C5 and the 2-rank shapes 3-25 % faster (profiles/r04i_c4knobs.txt, r04j_c4knobs.txt;
-// 128 and 64 KiB lose again).  Connections between GPUs keep the reference's size.
+// 128 and 64 KiB lose again).  Connections between GPUs keep the reference's size, and so does a
+// communicator with a Simple schedule that sends more than two chunks before it receives
+// (init.cc: applySplits).
 constexpr int64_t kLocalSimpleBuff = 256 << 10;
 
 int refTypeSize(int dtype);

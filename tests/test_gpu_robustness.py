@@ -155,6 +155,27 @@ def test_sender_and_receiver_cut_the_same_fifo_steps():
         _allreduce_case(cr, 512 * 1000, 7, 78, "8n simple 2 MiB", ulp_bound=False)
 
 
+@pytest.mark.parametrize("case", ["ring", "rccl_8n", "env"])
+def test_local_simple_fifo_size(tmp_path, monkeypatch, case):
+    """Ranks on one GPU take 32-KiB Simple slots (plan.h: kLocalSimpleBuff) unless a Simple
+    schedule sends more than two chunks before it receives (RCCL's 8-rank all-pairs: the
+    reference's 512-KiB slots) or NCCL_BUFFSIZE is set; either way the results stay bit-exact."""
+    from tests.test_gpu_configs import _allreduce_case
+    if case == "rccl_8n":
+        p = os.path.join(RCCL, "allreduce-allpairs-8n-simple.xml")
+        if not os.path.exists(p):
+            pytest.skip("fixture missing")
+        xml, n, want = open(p).read(), 8, 512 << 10
+    else:
+        xml, n, want = xmlgen.allreduce_ring(4, 4, "Simple", True, 0, 1 << 40), 4, 32 << 10
+    if case == "env":
+        monkeypatch.setenv("NCCL_BUFFSIZE", str(1 << 20))
+        want = (1 << 20) // 8
+    with CoResident(n, [xml], str(tmp_path)) as cr:
+        assert all(c.info()["simpleSlotBytes"] == want for c in cr.comms)
+        _allreduce_case(cr, 512 * 1024, 7, 5, "local fifo %s" % case, ulp_bound=False)
+
+
 def test_calls_beyond_2gib():
     """2.4 GB per rank (600 M floats): user buffers beyond a buffer descriptor's 2 GiB reach and
     offsets beyond 2^31 elements' bytes, through an all-pairs Simple schedule and through the ring
