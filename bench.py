@@ -157,7 +157,7 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
     ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
     for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
     inst_large.  At more ranks: rank-ordered one-shot (4 instances; lowered to the one-hop fold)
-    below 128 KiB, then two-phase all-pairs with inst_large instances."""
+    below 64 KiB, then two-phase all-pairs with inst_large instances."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
         # "O" = rank-ordered one-shot, "p" = 2-rank one-hop exchange (s, rrc), "r" = ring with
@@ -175,12 +175,13 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         # 32 MiB 398 -> 450 GB/s
         spec = [(0, 4 << 10, 1, "p"), (4 << 10, (1 << 30) + 1, inst_large, "p")]
     else:
-        # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 128 KiB: the
+        # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 64 KiB: the
         # runtime lowers it to the one-hop fold there (msccl_amd/csrc/lower.cc), which beats the
         # two-phase all-pairs up to that size (8 ranks, fp16, graph replay: 16 KiB 18.8 -> 12.7 us,
-        # 64 KiB 23.1 -> 16.0, 128 KiB 24.2 -> 24.0; profiles/r04b_xover.txt); it moves (n-1) S per
-        # rank, so the two-phase schedule takes over above
-        spec = [(0, 128 << 10, 4, "O"), (128 << 10, (1 << 30) + 1, inst_large)]
+        # 64 KiB 23.1 -> 16.0; profiles/r04b_xover.txt); the two-phase schedule takes over above
+        # (lowered too at 64 KiB, interpreted from 128 KiB: 18.4 us there against the fold's 24.5,
+        # profiles/r04l_sweep.txt)
+        spec = [(0, 64 << 10, 4, "O"), (64 << 10, (1 << 30) + 1, inst_large)]
     tiers = []
     for k, t in enumerate(spec):
         lo, hi, inst = t[:3]
