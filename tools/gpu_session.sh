@@ -72,18 +72,16 @@ for c, d in json.load(open('${O}_c4k.json'))['configs'].items():
           if isinstance(v, dict) and 'kernel_ms' in v), d.get('verified'), d.get('error', ''))" | tee -a ${O}_c4knobs.txt
     done ;;
   xcdpmc)
-    # per-XCD memory requests of the C2 headline launch: the counters' dimensions, then one pass
-    # with the per-instance output kept (JSON)
+    # per-XCD TCC counters of the C2 headline launch (JSON keeps every TCC instance x XCC value):
+    # requests, read latency (RDREQ_LEVEL / RDREQ), DRAM credit stalls, hits / misses per XCD
     timeout -s KILL 60 rocprofv3 -L > ${O}_counters.txt 2>&1 || fail "rocprofv3 -L" ${O}_counters.txt
-    for c in TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_HIT TCC_MISS; do
-      timeout -s KILL 120 rocprofv3 --pmc $c --output-format json csv -d gpurun_out/${TAG}_xcd_$c -o run -- \
+    for c in ${XCDCOUNTERS:-TCC_EA0_RDREQ TCC_EA0_RDREQ_LEVEL TCC_EA0_WRREQ TCC_EA0_RDREQ_DRAM_CREDIT_STALL TCC_HIT TCC_MISS}; do
+      d=gpurun_out/${TAG}_xcd_$c
+      timeout -s KILL 120 rocprofv3 --pmc $c --output-format json -d $d -o run -- \
         python3 bench.py --sizes 33554432 --steps 10 --warmup 3 --no-cpu --quiet --no-secondary --pmc off --extras "" --eager \
         > /dev/null 2> ${O}_xcd_$c.err || fail "xcdpmc $c" ${O}_xcd_$c.err
-      # keep a summary and the head of the JSON (its per-dimension layout), not the raw output
-      d=gpurun_out/${TAG}_xcd_$c
-      { for f in $(find $d -name "*counter_collection.csv"); do head -3 $f; wc -l $f; done
-        for f in $(find $d -name "*.json"); do echo "== $f $(wc -c < $f) bytes"; head -c 150000 $f; echo; done
-      } > ${O}_xcd_$c.txt 2>&1
+      python3 tools/xcd_pmc.py $(find $d -name "*results.json" | head -1) > ${O}_xcd_$c.txt 2>&1 || fail "xcd_pmc $c" ${O}_xcd_$c.txt
+      cat ${O}_xcd_$c.txt
       rm -rf $d
     done ;;
   prof)
