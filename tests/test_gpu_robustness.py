@@ -241,7 +241,7 @@ def test_simple_handoff_uneven_load_l1_warm():
     xml = _uneven_pair_xml(8, 6)
     algos = [L.parse_xml(xml, r, 2) for r in range(2)]
     assert len(algos[0].tbs[0].transfers) == 8 and len(algos[1].tbs[0].transfers) == 2
-    # 8 chunks of 64 Ki int32: several 512-KiB FIFO slots per transfer
+    # 8 chunks of 64 Ki int32: 8 of the local 32-KiB FIFO slots per chunk (plan.h: kLocalSimpleBuff)
     gpu, ora, _ = run_collective(xml, 2, L.ALLREDUCE, 8 * (1 << 16), 2, 0, True, seed=77, iters=200)
     for r in range(2):
         assert np.array_equal(gpu[r].view(np.uint32), ora[r].view(np.uint32)), describe_mismatch(gpu[r], ora[r])
