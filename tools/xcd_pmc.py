@@ -34,9 +34,15 @@ def main():
     names = {}      # kernel id -> name
     counters = {}   # counter id -> name
 
+    order = {}      # counter id -> dimensions of its instances, in the listed order
+
     def reg(o):
         if "instance_id" in o and isinstance(o.get("dimensions"), list):
             dims[o["instance_id"]] = {d.get("dimension_name"): d.get("index") for d in o["dimensions"] if isinstance(d, dict)}
+        if isinstance(o.get("instances"), list) and "id" in o:
+            cid = o["id"]["handle"] if isinstance(o["id"], dict) else o["id"]
+            order[cid] = [{d.get("dimension_name"): d.get("index") for d in x.get("dimensions", [])}
+                          for x in o["instances"] if isinstance(x, dict)]
         if "kernel_id" in o and any(k in o for k in ("kernel_name", "truncated_kernel_name", "formatted_kernel_name")):
             names[o["kernel_id"]] = o.get("kernel_name") or o.get("formatted_kernel_name") or o.get("truncated_kernel_name")
         if "id" in o and "name" in o and ("block" in o or "description" in o):
@@ -62,13 +68,20 @@ def main():
         walk({k: v for k, v in o.items() if k != "records"}, find)
         if kid is None or a.kernel not in str(names.get(kid, "")):
             return
-        for r in recs:
+        for i, r in enumerate(recs):
             seen_keys.update(r.keys())
-            iid = r.get("instance_id", r.get("id"))
+            iid = r.get("instance_id")
             if isinstance(iid, dict):
                 iid = iid.get("handle")
             v = r.get("counter_value", r.get("value"))
-            d = dims.get(iid)
+            cid = r.get("counter_id")
+            if isinstance(cid, dict):
+                cid = cid.get("handle")
+            # records without an instance id come in the order of the counter's "instances" list
+            if iid is not None:
+                d = dims.get(iid)
+            else:
+                d = order[cid][i] if len(order.get(cid, ())) == len(recs) else None
             if d is None or v is None:
                 continue
             per[did][d.get("DIMENSION_XCC", 0)] += float(v)
