@@ -191,26 +191,21 @@ struct RankWork {
   int64_t sizePerChunk;         // sizePerMscclChunk = count*sizeMultiplier/nchunksPerLoop (elements)
   int64_t chunkSize;            // interpreter chunkSize (elements)
   int64_t minChunk;             // LL: nthreads*8/sizeof(T); Simple: rounding unit (nthreads-32)*8/sizeof(T)
-  // Every field below is a whole dword: sub-dword kernel arguments at offsets that are not
-  // dword-aligned were loaded with vector loads (global_load_ushort / _sbyte) ahead of the rank
-  // lookup, a memory round trip a scalar load from the argument block does not pay
   uint32_t launchSeq;            // host launch counter (diagnostics only; flags use DevComm::epoch)
-  int32_t blockBase;
-  int32_t nBlocks;              // workgroups = XML thread blocks x split
-  int32_t refNthreads;          // reference nthreads (small-reduce switch, chunk rounding)
-  int32_t maxAllowedCount;
-  int32_t split;                // workgroups per XML thread block; each owns 1/split of every op
-  int32_t merge;                // full interpreter iterations run as one (same per-element operations)
-  int32_t foldPeers;            // flat tree (mscclFoldKernel): peers, on the records of thread blocks 1..foldPeers
-  int32_t epochSlots;           // the schedule's flag / epoch slots (flags and epochs point at its range)
-  int32_t pad1;
+  int16_t blockBase;
+  int16_t nBlocks;              // workgroups = XML thread blocks x split
+  int16_t refNthreads;          // reference nthreads (small-reduce switch, chunk rounding)
+  uint8_t maxAllowedCount;
+  uint8_t split;                // workgroups per XML thread block; each owns 1/split of every op
+  uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
+  uint8_t foldPeers;            // flat tree (mscclFoldKernel): peers, on the records of thread blocks 1..foldPeers
+  int16_t epochSlots;           // the schedule's flag / epoch slots (flags and epochs point at its range)
   int64_t maxOpElems;           // largest run of sends before a receive (elements, all sub-connections)
   // ring fallback (kRingNone for MSCCL schedules): the program's offsets are chunk / rank indices
   // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)
-  int32_t ringColl;
-  int32_t ringRanks;
+  uint8_t ringColl;
+  int16_t ringRanks;
   int32_t foldChunkPacks;       // a lowered schedule folding chunks in several orders: packs per chunk (else 0)
-  int32_t pad2;
   int64_t ringSize;             // elements of one rank's block (args->count)
   int64_t ringLastChunk;        // LL ReduceScatter / AllGather lastChunkSize (enqueue.cc:653-658)
   // copies of per-communicator constants (kernel arguments: no dependent DevComm load)
@@ -231,7 +226,7 @@ struct LaunchArgsN {
 };
 using LaunchArgs = LaunchArgsN<kMaxLaunchRanks>;
 // A launch of at most two ranks (one rank per process, or the 2-rank co-resident C2 launch) takes
-// a kernel whose argument block holds two RankWorks (488 B instead of 3.8 KiB): the HIP runtime
+// a kernel whose argument block holds two RankWorks (424 B instead of 3.3 KiB): the HIP runtime
 // copies the whole block per launch, about 0.9 us more for the larger one (tools/host_lat).
 constexpr int kCompactLaunchRanks = 2;
 

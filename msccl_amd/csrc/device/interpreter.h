@@ -1837,7 +1837,7 @@ __device__ __forceinline__ void warmArgLines(const void* p) {
 
 // The RankWork of block b, its lines warmed after the lookup in the launches of more than
 // kCompactLaunchRanks ranks (8 ranks: 0.2-0.35 us less per launch).  The compact launches do
-// without: warming their whole argument block first cost 0.2-0.5 us (profiles/r04f_lat.txt).
+// without: warming their whole 424-B block first cost 0.2-0.5 us (profiles/r04f_lat.txt).
 template <int R>
 __device__ __forceinline__ const RankWork& rankWorkOf(const LaunchArgsN<R>& args, int b) {
   const RankWork& w = args.w[rankOfBlock(args, b)];
