@@ -13,6 +13,7 @@
 #   xover     the lowered fold against the interpreter, 8 KiB - 128 KiB (MSCCL_AMD_LOWER_MAX_BYTES)
 #   c4trace   where the 8-rank C4 ring launch waits (tools/trace_report.py --summary)
 #   c4knobs   the 8-rank C4 shape under each environment of C4ENVS (';'-separated)
+#   c3inst    the 8-rank C3 shape at 32 MiB for each all-pairs instance count in C3INST, and its trace
 #   xcdpmc    rocprofv3's counter list and per-instance TCC request counters of the C2 launch
 #   prof      tools/profile.sh on the C2 headline (kernel stats, FETCH_SIZE, WRITE_SIZE)
 #   prof8     the same on the 8-rank C3 shape and C4 / C5 (per-kernel traffic)
@@ -60,6 +61,17 @@ for step in $STEPS; do
     MSCCL_AMD_TRACE=1 timeout -k 10 300 python3 tools/trace_report.py --schedule ring --ranks 8 --instances 32 --proto Simple \
       --dtype 9 --bytes 268435456 --iters 3 --summary > ${O}_c4trace.txt 2>&1 || fail c4trace ${O}_c4trace.txt
     cat ${O}_c4trace.txt ;;
+  c3inst)
+    for i in ${C3INST:-2 4 8}; do
+      env $C3ENV timeout -k 10 300 python3 bench.py --vranks 8 --dtype fp16 --sizes 33554432 --instances $i --no-cpu --pmc off \
+        --no-secondary > ${O}_c3i.json 2>> ${O}_c3i.err || fail "c3inst $i" ${O}_c3i.err
+      python3 -c "
+import json; d = json.load(open('${O}_c3i.json')); s = d['sweep'][-1]
+print('C3 32 MiB instances $i $C3ENV', s['kernel_ms'], s['busbw'], s['kernel'])" | tee -a ${O}_c3inst.txt
+    done
+    MSCCL_AMD_TRACE=1 timeout -k 10 300 python3 tools/trace_report.py --schedule allpairs --ranks 8 --instances 4 --proto LL \
+      --dtype 6 --bytes 33554432 --iters 3 --summary > ${O}_c3trace.txt 2>&1 || fail c3trace ${O}_c3trace.txt
+    cat ${O}_c3trace.txt ;;
   c4knobs)
     IFS=';' read -ra EV <<< "${C4ENVS:-NCCL_BUFFSIZE=4194304}"
     for e in "${EV[@]}"; do
