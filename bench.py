@@ -633,7 +633,10 @@ def main():
     dt = M.DTYPE_NAMES[dtname]
     ts = M.TYPE_SIZE[dt]
     proto_id = {"LL": 0, "LL128": 1, "Simple": 2}[a.proto]
-    inst = a.instances or (16 if n <= 2 else (8 if n <= 4 else 4))
+    # all-pairs instances of the large tier: 8 up to 8 ranks (8 co-resident ranks, fp16 32 MiB:
+    # 2 / 4 / 8 instances 0.60 / 0.62 / 0.52 ms, 16 exceeds the 512 co-resident workgroups,
+    # profiles/r04n_c3inst.txt); beyond, as many as keep n (n - 1) thread blocks within 512
+    inst = a.instances or (16 if n <= 2 else 8 if n <= 8 else max(1, 512 // (n * (n - 1))))
     sizes = [int(s) for s in a.sizes.split(",")] if a.sizes else SIZES
     tmp = os.environ.get("TMPDIR", "/tmp")
     tiers = make_xmls(n, a.proto, inst, tmp, a.tiers)
