@@ -157,7 +157,7 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
     ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
     for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
     inst_large.  At more ranks: rank-ordered one-shot (4 instances; lowered to the one-hop fold)
-    below 64 KiB, then two-phase all-pairs with inst_large instances."""
+    below 64 KiB, then two-phase all-pairs with 4 instances below 4 MiB and inst_large above."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
         # "O" = rank-ordered one-shot, "p" = 2-rank one-hop exchange (s, rrc), "r" = ring with
@@ -181,7 +181,10 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         # 64 KiB 23.1 -> 16.0; profiles/r04b_xover.txt); the two-phase schedule takes over above
         # (lowered too at 64 KiB, interpreted from 128 KiB: 18.4 us there against the fold's 24.5,
         # profiles/r04l_sweep.txt)
-        spec = [(0, 64 << 10, 4, "O"), (64 << 10, (1 << 30) + 1, inst_large)]
+        # two instance counts: up to 4 below 4 MiB (8 ranks: 128 KiB 17.9 against 21.1 us with 8,
+        # 512 KiB 24.1 against 26.5), inst_large from 4 MiB (32 MiB 538 against 570 us,
+        # profiles/r04o_c3_inst.txt)
+        spec = [(0, 64 << 10, 4, "O"), (64 << 10, 4 << 20, min(4, inst_large)), (4 << 20, (1 << 30) + 1, inst_large)]
     tiers = []
     for k, t in enumerate(spec):
         lo, hi, inst = t[:3]
