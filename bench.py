@@ -311,9 +311,12 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
         xmls = {"ar": xmlgen.allreduce_ring(n, chans, "Simple", True, 0, 1 << 40, name="c4_ring")}
         dt, S = M.BFLOAT16, 256 << 20
     elif cfg == "C5":
-        # 2 ranks: 16 instances (RS 126 -> 243, AG 225 -> 373 GB/s against 4); more ranks: 4, so
-        # n (n-1) x instances thread blocks stay resident when the ranks share one GPU
-        c5i = int(os.environ.get("MSCCL_AMD_BENCH_C5_INSTANCES", "0")) or (16 if n <= 2 else 4)
+        # 2 ranks: 16 instances (RS 126 -> 243, AG 225 -> 373 GB/s against 4); up to 8 ranks: 8
+        # (8 co-resident ranks: AG 0.280 against 0.298 ms with 4, RS within noise,
+        # profiles/r04r_c4knobs.txt); beyond, as many as keep n (n - 1) x instances thread blocks
+        # resident when the ranks share one GPU
+        c5i = int(os.environ.get("MSCCL_AMD_BENCH_C5_INSTANCES", "0")) or (
+            16 if n <= 2 else 8 if n <= 8 else max(1, 512 // (n * (n - 1))))
         rs_form = os.environ.get("MSCCL_AMD_BENCH_RS_FORM", "chain")   # "scratch": the round-2 form
         xmls = {"rs": xmlgen.reduce_scatter_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_rs", form=rs_form),
                 "ag": xmlgen.allgather_allpairs(n, c5i, "Simple", False, 0, 1 << 40, name="c5_ag")}
