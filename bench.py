@@ -179,8 +179,7 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         # runtime lowers it to the one-hop fold there (msccl_amd/csrc/lower.cc), which beats the
         # two-phase all-pairs up to that size (8 ranks, fp16, graph replay: 16 KiB 18.8 -> 12.7 us,
         # 64 KiB 23.1 -> 16.0; profiles/r04b_xover.txt); the two-phase schedule takes over above
-        # (lowered too at 64 KiB, interpreted from 128 KiB: 18.4 us there against the fold's 24.5,
-        # profiles/r04l_sweep.txt)
+        # (lowered too up to 128 KiB: profiles/r04t_lat.txt)
         # two instance counts: up to 4 below 4 MiB (8 ranks: 128 KiB 17.9 against 21.1 us with 8,
         # 512 KiB 24.1 against 26.5), inst_large from 4 MiB (32 MiB 538 against 570 us,
         # profiles/r04o_c3_inst.txt)

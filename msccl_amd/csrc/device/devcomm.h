@@ -35,7 +35,11 @@ constexpr int kFlagStride = 4;         // uint64 words per flag (32 B, mscclFlag
 constexpr int kMaxSplit = 8;           // workgroups per XML thread block (sub-connections)
 constexpr int kNT = 512;               // threads per workgroup (8 waves of 64)
 constexpr int kMaxFoldPeers = 15;      // flat tree fold: peers of one rank (MSCCL_MAX_REDUCE_FUSION 16 ranks)
-constexpr int kFlatSubs = 4;           // flat tree: sub-connections per peer = most fold workgroups per rank
+// flat tree: sub-connections per peer = most fold workgroups per rank.  16: one 16-B pack per
+// lane up to 128 KiB (fp16 / bf16) per rank; with 4, a 128-KiB 8-rank fold took 23.3 us against
+// 12.5 (lanes walking 4 packs, each poll waiting for the last), 64 KiB 15.6 against 11.3, small
+// calls unchanged (profiles/r04t_lat.txt).  LL FIFOs only: 8 MiB per peer
+constexpr int kFlatSubs = 16;
 constexpr int kFoldPacksPerWg = 512;   // flat tree: a fold workgroup per 512 packs (8 KiB) of the call
 constexpr int kMaxFoldClasses = 16;    // lowered schedules (lower.cc): fold orders per schedule
 constexpr int kMaxFoldChunks = 1024;   // lowered schedules with several orders: chunks per loop

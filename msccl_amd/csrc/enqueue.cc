@@ -224,7 +224,7 @@ RankWork makeFlatWork(Planned& p) {
   w.minChunk = p.plan.minChunk;
   // workgroups per rank: one per kFoldPacksPerWg packs of the call, at most kFlatSubs (a function
   // of the call's size alone, so every rank picks the same and the two ends of every
-  // sub-connection own the same packs; one workgroup against up to four: profiles/r03_ab_fold_wgs_and_r02.txt)
+  // sub-connection own the same packs; one workgroup against up to four: profiles/r03_ab_fold_wgs_and_r02.txt; 16 against 4: r04t_lat.txt)
   const int64_t pe = 16 / refTypeSize(p.plan.dtype);
   const int64_t npk = (p.plan.sizePerChunk + pe - 1) / pe;
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(kFlatSubs, (npk + kFoldPacksPerWg - 1) / kFoldPacksPerWg));

@@ -286,10 +286,10 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
 int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p) {
   // Where the fold beats the interpreted schedule (co-resident ranks, graph replay,
   // profiles/r04b_xover.txt, r04l_sweep.txt): 2 ranks up to a few KiB (the exchange-set kernel
-  // runs the pair exchange itself in ~6.6 us from 8 KiB on), 8 ranks up to 64 KiB (the one-shot
-  // 16 KiB 20.2 -> 12.7 us, 64 KiB 23.9 -> 16.0; at 128 KiB the interpreted two-phase all-pairs
-  // x16 takes 18.4 us, its fold 24.5)
-  const int64_t limit = k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : c.nRanks <= 2 ? (int64_t)(4 << 10) : (int64_t)(64 << 10);
+  // runs the pair exchange itself in ~6.6 us from 8 KiB on), 8 ranks up to 128 KiB (16 fold
+  // workgroups per rank, profiles/r04t_lat.txt: the one-shot 64 KiB 23.7 -> 11.3 us, the two-phase
+  // all-pairs 128 KiB 17.9-21.1 -> 13.1; at 256 KiB 21.6 against 21.2, even)
+  const int64_t limit = k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : c.nRanks <= 2 ? (int64_t)(4 << 10) : (int64_t)(128 << 10);
   if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > limit ||
       p->nBytes > (1ll << 30))
     return 1;
