@@ -131,7 +131,8 @@ def test_rccl_allpairs_lowered_with_chunk_classes(tmp_path, nbytes):
 
 
 @pytest.mark.parametrize("n,count,dt,lowered", [(8, 2 * 64 * 8 * 8, 6, True), (4, 16 * 40, 7, True),
-                                                 (4, 16 * 41, 7, False)])
+                                                 (4, 16 * 41, 7, False),
+                                                 (8, 64 * 1024, 6, True)])   # 128 KiB: 16 fold workgroups
 def test_allpairs_classes_and_whole_packs(tmp_path, n, count, dt, lowered):
     """The two-phase all-pairs: lowered when every chunk is whole 16-B packs (a pack folds in one
     chunk's order); 41 floats per chunk are not, and the call keeps the interpreter."""
