@@ -151,13 +151,14 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only:
     return int(round(hbm)), int(round(wire))
 
 
-def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
+def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None, remote: bool = False):
     """All-pairs schedules in size tiers, as a user registers several msccl-tools XMLs with
     minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
     ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
     for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
     inst_large.  At more ranks: rank-ordered one-shot (4 instances; lowered to the one-hop fold)
-    below 64 KiB, then two-phase all-pairs with 4 instances below 4 MiB and inst_large above."""
+    below 64 KiB, then two-phase all-pairs with 4 instances below 4 MiB and inst_large above.
+    remote (one rank per GPU, peers over xGMI): inst_large from 64 KiB on."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
         # "O" = rank-ordered one-shot, "p" = 2-rank one-hop exchange (s, rrc), "r" = ring with
@@ -183,7 +184,11 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None):
         # two instance counts: up to 4 below 4 MiB (8 ranks: 128 KiB 17.9 against 21.1 us with 8,
         # 512 KiB 24.1 against 26.5), inst_large from 4 MiB (32 MiB 538 against 570 us,
         # profiles/r04o_c3_inst.txt)
-        spec = [(0, 64 << 10, 4, "O"), (64 << 10, 4 << 20, min(4, inst_large)), (4 << 20, (1 << 30) + 1, inst_large)]
+        # profiles/r04o_c3_inst.txt).  Those counts are set by 8 ranks sharing one GPU's CUs; with
+        # one rank per GPU a rank's workgroups have its GPU to themselves and each thread block
+        # drives one xGMI link, so the mid tier takes inst_large too (8 thread blocks per link)
+        mid = inst_large if remote else min(4, inst_large)
+        spec = [(0, 64 << 10, 4, "O"), (64 << 10, 4 << 20, mid), (4 << 20, (1 << 30) + 1, inst_large)]
     tiers = []
     for k, t in enumerate(spec):
         lo, hi, inst = t[:3]
@@ -644,7 +649,9 @@ def main():
     inst = a.instances or (16 if n <= 2 else 8 if n <= 8 else max(1, 512 // (n * (n - 1))))
     sizes = [int(s) for s in a.sizes.split(",")] if a.sizes else SIZES
     tmp = os.environ.get("TMPDIR", "/tmp")
-    tiers = make_xmls(n, a.proto, inst, tmp, a.tiers)
+    # peers on other GPUs: one rank per process and GPU (not the one-GPU rehearsal)
+    remote = mode == "rank" and os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") != "1"
+    tiers = make_xmls(n, a.proto, inst, tmp, a.tiers, remote=remote)
     os.environ["MSCCL_XML_FILES"] = ":".join(t[3] for t in tiers)
     os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "30")
 

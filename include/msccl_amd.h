@@ -32,11 +32,24 @@ int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, si
  * {"ok":0,"why":"..."}.  No GPU needed. */
 int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen);
 
-/* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the launch plan
- * (enqueue.cc:591-734).  coll uses ncclFunc_t numbering (AllGather=2, ReduceScatter=3,
+/* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the schedule's chunk
+ * plan (enqueue.cc:591-734), the reference's computeColl field by field, from the environment
+ * alone: not init's decisions (lowering to the fold, the local Simple FIFO; see
+ * mscclAmdLaunchPlanJson).  coll uses ncclFunc_t numbering (AllGather=2, ReduceScatter=3,
  * AllReduce=4).  Writes JSON {"algo":i,...} or {"algo":-1}.  No GPU needed. */
 int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_t count, int dtype,
                      int redop, int inPlace, char* out, size_t outLen);
+
+/* What a communicator of `nranks` ranks launches for one call, with init's decisions: all ranks
+ * on one GPU (oneGpu = 1) or spread over GPUs (oneGpu = 0: every rank has peers over xGMI).  The
+ * same planning function as the communicator's (plan.cc: planCall) on the same inputs: the
+ * schedules, the one-hop lowering and its size limit (co-resident: measured; across GPUs: the
+ * link model), the Simple FIFO size, the fallback.  JSON {"kernel": "fold" |
+ * "interpreter" | "ring" | "tree", "algo", "proto", "lowered", "nBytes", "lowerMaxBytes",
+ * "simpleBuffBytes", "remote", "classes": [fold orders per algorithm, 0 = not lowered]}.
+ * No GPU needed. */
+int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGpu, int coll, size_t count,
+                           int dtype, int redop, int inPlace, char* out, size_t outLen);
 
 /* Communicator summary as JSON (algorithms, connections, scratch, FIFO geometry). */
 int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen);

@@ -89,6 +89,8 @@ def lib() -> ctypes.CDLL:
     if hasattr(L, "mscclAmdLowerJson"):  # MSCCL_AMD_LIB may name an older build (A/B runs)
         L.mscclAmdLowerJson.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, sz]
     L.mscclAmdPlanJson.argtypes = [ctypes.c_char_p, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
+    if hasattr(L, "mscclAmdLaunchPlanJson"):  # MSCCL_AMD_LIB may name an older build (A/B runs)
+        L.mscclAmdLaunchPlanJson.argtypes = [ctypes.c_char_p, i, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
     L.mscclAmdCommInfo.argtypes = [vp, ctypes.c_char_p, sz]
     L.mscclAmdNpkitDump.argtypes = [vp, ctypes.c_char_p]
     L.mscclAmdBootstrapAllgather.argtypes = [ctypes.POINTER(UniqueId), i, i, vp, sz, vp]
@@ -178,6 +180,17 @@ def plan_json(xml_files: str, rank: int, nranks: int, coll: int, count: int, dty
     buf = ctypes.create_string_buffer(1 << 16)
     _check(lib().mscclAmdPlanJson(xml_files.encode(), rank, nranks, coll, count, dtype, op, int(in_place), buf,
                                   len(buf)), "mscclAmdPlanJson")
+    return json.loads(buf.value.decode())
+
+
+def launch_plan_json(xml_files: str, rank: int, nranks: int, one_gpu: bool, coll: int, count: int, dtype: int,
+                     op: int, in_place: bool) -> dict:
+    """What a communicator launches for one call with init's decisions (plan.cc: planCall): ranks
+    all on one GPU (one_gpu) or spread over GPUs; {"kernel", "lowered", "lowerMaxBytes",
+    "simpleBuffBytes", ...} (include/msccl_amd.h: mscclAmdLaunchPlanJson)."""
+    buf = ctypes.create_string_buffer(1 << 16)
+    _check(lib().mscclAmdLaunchPlanJson(xml_files.encode(), rank, nranks, int(one_gpu), coll, count, dtype, op,
+                                        int(in_place), buf, len(buf)), "mscclAmdLaunchPlanJson")
     return json.loads(buf.value.decode())
 
 

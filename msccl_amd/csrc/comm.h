@@ -91,6 +91,8 @@ struct ncclComm {
                                                             // (both ends of the exchange agreed at init)
   int maxSplit = 1;                // sub-connections per (channel, peer)
   int coResident = 1;              // ranks of this communicator on this rank's GPU
+  std::vector<int> foldClasses;    // per algorithm: algoFold's class count (0: not lowered)
+  msccl::PlanContext planCtx;      // what planCall reads (set at the end of init: commFinish)
 
   // transport
   std::vector<msccl::ConnKey> sendKeys, recvKeys;

@@ -131,6 +131,65 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
   return putOut(o.str(), out, outLen);
 }
 
+int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGpu, int coll, size_t count, int dtype,
+                           int redop, int inPlace, char* out, size_t outLen) {
+  if (rank < 0 || nranks < 2 || rank >= nranks) return ncclInvalidArgument;
+  // init's decisions for a communicator of nranks ranks, all on one GPU (oneGpu) or spread over
+  // several (every rank then has a peer on another GPU): the schedules as this rank loads them,
+  // the knobs, the one-hop lowering (lower.cc, on every rank's load; offered only where every
+  // rank offers it, which the same environment does), the Simple FIFO size (applySplits)
+  std::vector<Algorithm> algos;
+  if (xmlFiles) loadAlgosFromXmlFiles(xmlFiles, &algos, kMaxChannels, rank, nranks);
+  Knobs k = Knobs::fromEnv();
+  const bool flat = k.ringFallback && k.treeFlat && nranks <= kMaxReduceFusion;
+  std::vector<int> classes(algos.size(), 0), sendRun(algos.size(), 1);
+  for (size_t a = 0; a < algos.size(); a++) {
+    for (int r = 0; r < nranks; r++) {
+      Algorithm ar;
+      if (loadAlgoFromXml(algos[a].path.c_str(), &ar, kMaxChannels, r, nranks) == 0)
+        sendRun[a] = std::max(sendRun[a], algoSendRunOf(ar));
+    }
+    const Algorithm& g = algos[a];
+    if (k.lower && flat && lowerOffered() && g.valid && g.coll == kAllReduce && g.proto == kProtoLL && !g.path.empty() &&
+        g.ngpus == nranks) {
+      const FoldLowering fl = lowerScheduleFile(g.path, nranks);
+      if (fl.ok) classes[a] = (int)fl.order.size();
+    }
+  }
+  if (useLocalSimpleFifo(oneGpu != 0, k, algos, sendRun)) k.buffSizes[kProtoSimple] = kLocalSimpleBuff;
+  std::vector<Registration> regs;
+  PlanContext pc;
+  pc.algos = &algos;
+  pc.regs = &regs;
+  pc.knobs = &k;
+  pc.foldClasses = &classes;
+  pc.flat = flat;
+  pc.ringFallback = k.ringFallback != 0;
+  pc.scratchSize = (size_t)-1;  // uncapped (MSCCL_AMD_MAX_SCRATCH is not modelled here)
+  CallDesc c;
+  c.coll = coll;
+  c.count = count;
+  c.dtype = dtype;
+  c.redop = redop;
+  c.nRanks = nranks;
+  c.rank = rank;
+  c.inPlace = inPlace != 0;
+  c.remote = oneGpu == 0;
+  Plan p;
+  const int res = planCall(pc, c, false, &p);
+  if (res != 0) return res;
+  const char* kernel = p.ringColl == kTreeFlat ? "fold"
+                       : p.ringColl == kTreeAllReduce ? "tree" : p.ringColl ? "ring" : "interpreter";
+  std::ostringstream o;
+  o << "{\"kernel\":\"" << kernel << "\",\"algo\":" << p.algoIndex << ",\"proto\":" << p.proto
+    << ",\"lowered\":" << (p.ringColl == kTreeFlat && p.algoIndex >= 0 ? 1 : 0) << ",\"nBytes\":" << p.nBytes
+    << ",\"lowerMaxBytes\":" << (k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : defaultLowerMaxBytes(nranks, c.remote))
+    << ",\"simpleBuffBytes\":" << k.buffSizes[kProtoSimple] << ",\"remote\":" << (c.remote ? 1 : 0) << ",\"classes\":[";
+  for (size_t a = 0; a < classes.size(); a++) o << (a ? "," : "") << classes[a];
+  o << "]}";
+  return putOut(o.str(), out, outLen);
+}
+
 int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
   if (!commValid(comm)) return ncclInvalidArgument;
   std::ostringstream o;

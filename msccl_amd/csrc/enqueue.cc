@@ -74,10 +74,6 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
     if (op.sendbuff == op.recvbuff) out->noop = true;
     return ncclSuccess;
   }
-  if (asyncMany && comm->knobs.referenceSelection && op.customAlgo >= 0) {
-    WARN("MSCCL algorithms is not supposed to be used in async mode!");  // enqueue.cc:448-451
-    return ncclInvalidUsage;
-  }
   CallDesc c;
   c.coll = op.coll;
   c.count = op.count;
@@ -87,61 +83,9 @@ ncclResult_t planOp(const CollOp& op, Planned* out, bool asyncMany) {
   c.rank = comm->rank;
   c.inPlace = inPlaceOf(op.coll, op.sendbuff, op.recvbuff, op.count, op.dtype, comm->rank);
   c.customAlgo = op.customAlgo;
+  c.remote = comm->anyRemote;
   out->inPlace = c.inPlace;
-  int idx = asyncMany && comm->knobs.referenceSelection ? -1 : selectAlgo(comm->algos, comm->regs, c, comm->knobs);
-  if (idx < 0) {
-    // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
-    if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
-      if (flatEnabled(comm)) makeFlatTreePlan(c, comm->knobs, &out->plan);
-      INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; %s fallback (%s, %d channels)",
-           op.coll, op.count, (int)op.dtype,
-           out->plan.ringColl == kTreeFlat ? "flat" : out->plan.ringColl == kTreeAllReduce ? "tree" : "ring",
-           out->plan.proto == kProtoLL ? "LL" : "Simple", out->plan.ringChannels);
-      return ncclSuccess;
-    }
-    WARN("MSCCL: no loaded algorithm matches coll=%d count=%zu type=%d op=%d inplace=%d nranks=%d "
-         "and the ring fallback %s", op.coll, op.count, (int)op.dtype, (int)op.op, (int)c.inPlace, comm->nRanks,
-         comm->ringFallback ? "does not support it" : "is disabled (MSCCL_AMD_RING_FALLBACK=0)");
-    return ncclInvalidUsage;
-  }
-  int protoOverride = -1;
-  for (auto& r : comm->regs)
-    if (r.algoIndex == idx) protoOverride = r.proto;
-  if ((protoOverride >= 0 ? protoOverride : comm->algos[idx].proto) == kProtoLL128 && comm->anyRemote &&
-      !comm->knobs.ll128Remote) {
-    // The CDNA4 LL128 line relies on a 16-B store arriving untorn.  That is observed for local
-    // HBM, not shown for xGMI peer stores; the reference likewise enables LL128 only where its
-    // line atomicity holds (tuning.cc:210-214).  Run the schedule with LL (same values for the
-    // commutative ops MSCCL admits) unless MSCCL_AMD_LL128_REMOTE=1.
-    static bool warned = false;
-    if (!warned) {
-      warned = true;
-      WARN("MSCCL: algorithm %s is LL128 and peers are on other GPUs; running it with LL "
-           "(MSCCL_AMD_LL128_REMOTE=1 keeps LL128)", comm->algos[idx].name.c_str());
-    }
-    protoOverride = kProtoLL;
-  }
-  NCCLCHECK(makePlan(comm->algos, idx, protoOverride, c, comm->knobs, &out->plan));
-  if ((size_t)idx < comm->algoFold.size() && !comm->algoFold[idx].order.empty() && flatEnabled(comm) &&
-      lowerToFoldPlan(c, comm->knobs, (int)comm->algoFold[idx].order.size(), &out->plan) == 0) {
-    // a one-hop schedule (lower.cc): the fold kernel computes its values in one hop
-    INFO(kSubColl, "MSCCL: %s count=%zu runs as the one-hop fold", comm->algos[idx].name.c_str(), op.count);
-    return ncclSuccess;
-  }
-  if (out->plan.scratchNeeded > comm->scratchSize) {
-    // The scratch is sized from the XMLs' maxBytes at init (init.cc:809-835), so this only
-    // happens when MSCCL_AMD_MAX_SCRATCH capped it.  The reference reports ncclInternalError
-    // (enqueue.cc:580-589); the capped schedule is treated as not matching instead.
-    if (comm->ringFallback && makeRingPlan(c, comm->knobs, &out->plan) == 0) {
-      if (flatEnabled(comm)) makeFlatTreePlan(c, comm->knobs, &out->plan);
-      INFO(kSubColl, "MSCCL: scratch %zu < %zu needed (MSCCL_AMD_MAX_SCRATCH); ring fallback", comm->scratchSize,
-           out->plan.scratchNeeded);
-      return ncclSuccess;
-    }
-    WARN("MSCCL: MSCCL scratch pad size is smaller than expected %zu < %zu", comm->scratchSize, out->plan.scratchNeeded);
-    return ncclInternalError;
-  }
-  return ncclSuccess;
+  return (ncclResult_t)planCall(comm->planCtx, c, asyncMany, &out->plan);
 }
 
 // Ring fallback: one workgroup per ring channel, the reference's runRing program in ring mode;

@@ -46,20 +46,12 @@ ncclResult_t loadAlgos(ncclComm* comm) {
 // then keeps a lowering only where every rank reached it (applySplits).
 void analyzeLowering(ncclComm* comm) {
   comm->algoFold.assign(comm->algos.size(), ncclComm::FoldProgram());
-  // NPKit logs the schedule's own primitives (msccl_interpreter.h's placement): a rank with the
-  // log on offers no lowering, and the init allgather then keeps the interpreter on every rank
-  if (!comm->knobs.lower || !flatEnabled(comm) || envInt("MSCCL_AMD_NPKIT", 0) > 0) return;
+  if (!comm->knobs.lower || !flatEnabled(comm) || !lowerOffered()) return;
   for (size_t g = 0; g < comm->algos.size(); g++) {
     const Algorithm& a = comm->algos[g];
-    if (!a.valid || a.coll != kAllReduce || a.proto != kProtoLL || a.path.empty()) continue;
-    std::vector<Algorithm> byRank(comm->nRanks);
-    bool loaded = true;
-    for (int r = 0; r < comm->nRanks && loaded; r++) {
-      if (r == comm->rank) byRank[r] = a;
-      else loaded = loadAlgoFromXml(a.path.c_str(), &byRank[r], kMaxChannels, r, comm->nRanks) == 0;
-    }
-    if (!loaded) continue;
-    const FoldLowering fl = analyzeFoldLowering(byRank);
+    // a schedule for another rank count is never selected (selectAlgo): nothing to decide
+    if (!a.valid || a.coll != kAllReduce || a.proto != kProtoLL || a.path.empty() || a.ngpus != comm->nRanks) continue;
+    const FoldLowering fl = lowerScheduleFile(a.path, comm->nRanks);
     if (fl.ok) {
       ncclComm::FoldProgram& f = comm->algoFold[g];
       f.chunkClass = fl.chunkClass;
@@ -225,10 +217,8 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   // two chunks before it receives: a call moves up to chunkSize = half the FIFO per chunk, and a
   // longer run of sends must fit the FIFO whole while its peer sends too (RCCL's 8-rank Simple
   // all-pairs sends 8 chunks first: it keeps the reference's size)
-  bool smallFifo = maxCo == (int)recs.size() && !comm->knobs.simpleBuffEnv;
-  for (size_t a = 0; a < comm->algos.size(); a++)
-    if (comm->algos[a].proto == kProtoSimple && comm->algoSendRun[a] > 2) smallFifo = false;
-  if (smallFifo) comm->knobs.buffSizes[kProtoSimple] = kLocalSimpleBuff;
+  if (useLocalSimpleFifo(maxCo == (int)recs.size(), comm->knobs, comm->algos, comm->algoSendRun))
+    comm->knobs.buffSizes[kProtoSimple] = kLocalSimpleBuff;
   // a schedule runs as the fold only when every rank found it one (the two ends of every flat
   // connection must run the same kernel)
   for (size_t a = 0; a < comm->algoFold.size() && a < (size_t)kMaxAlgos; a++)
@@ -281,6 +271,17 @@ static ncclResult_t allocSlots(ncclComm* comm) {
 }
 
 ncclResult_t commFinish(ncclComm* comm) {
+  comm->foldClasses.assign(comm->algos.size(), 0);
+  for (size_t a = 0; a < comm->algoFold.size() && a < comm->algos.size(); a++)
+    comm->foldClasses[a] = (int)comm->algoFold[a].order.size();
+  PlanContext& pc = comm->planCtx;
+  pc.algos = &comm->algos;
+  pc.regs = &comm->regs;
+  pc.knobs = &comm->knobs;
+  pc.foldClasses = &comm->foldClasses;
+  pc.flat = flatEnabled(comm);
+  pc.ringFallback = comm->ringFallback;
+  pc.scratchSize = comm->scratchSize;
   NCCLCHECK(algoUpload(comm));
   NCCLCHECK(allocSlots(comm));
   DevComm dc;

@@ -31,13 +31,17 @@
 // schedule that deadlocks, leaves FIFO messages, reads an uninitialised chunk into the result,
 // folds chunks in a tree shape or in orders that differ between chunks of one rank) is not
 // lowered.
+#include <stdio.h>
+
 #include <algorithm>
 #include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <vector>
 
 #include "comm.h"
+#include "debug.h"
 #include "lower.h"
 
 namespace msccl {
@@ -279,6 +283,45 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
   if (out.order.size() > 1 && C > kMaxFoldChunks) return fail("more chunks than the fold kernel's class map holds");
   out.ok = true;
   return out;
+}
+
+bool lowerOffered() {
+  // NPKit and the full trace (MSCCL_AMD_TRACE=1) record the schedule's own primitives
+  // (msccl_interpreter.h's placement): a rank with either on offers no lowering, and the init
+  // allgather then keeps the interpreter on every rank, so a traced schedule runs as written
+  return envInt("MSCCL_AMD_NPKIT", 0) <= 0 && envInt("MSCCL_AMD_TRACE", 0) != 1;
+}
+
+FoldLowering lowerScheduleFile(const std::string& path, int nRanks) {
+  // the file's text and the rank count are the key: a path may be rewritten between
+  // communicators of one process (a bench writes its tier files again under the same names)
+  std::string text;
+  if (FILE* f = fopen(path.c_str(), "rb")) {
+    char buf[65536];
+    size_t got;
+    while ((got = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, got);
+    fclose(f);
+  }
+  static std::mutex mu;
+  static std::map<std::pair<std::string, int>, FoldLowering> cache;
+  const auto key = std::make_pair(text, nRanks);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  FoldLowering fl;
+  std::vector<Algorithm> byRank(nRanks);
+  for (int r = 0; r < nRanks; r++)
+    if (loadAlgoFromXml(path.c_str(), &byRank[r], kMaxChannels, r, nRanks) != 0) {
+      fl.why = "the schedule does not load for rank " + std::to_string(r);
+      return fl;
+    }
+  fl = analyzeFoldLowering(byRank);
+  std::lock_guard<std::mutex> g(mu);
+  if (cache.size() > 256) cache.clear();  // a bound for long-lived processes
+  cache.emplace(key, fl);
+  return fl;
 }
 
 }  // namespace msccl

@@ -22,5 +22,13 @@ struct FoldLowering {
   std::vector<std::vector<std::vector<int>>> order;
 };
 FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank);
+// The schedule file at `path` loaded for each of nRanks ranks, then analyzeFoldLowering; cached
+// per process by (file text, nRanks), so the co-resident communicators of one process (each
+// rank loads it for every rank) parse and analyse a file once.  A file that does not load for
+// some rank is not lowered.
+FoldLowering lowerScheduleFile(const std::string& path, int nRanks);
+// false when this rank records the schedule's own primitives (MSCCL_AMD_NPKIT, MSCCL_AMD_TRACE=1):
+// it then offers no lowering at init, and every rank keeps the interpreter
+bool lowerOffered();
 
 }  // namespace msccl

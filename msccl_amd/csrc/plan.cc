@@ -87,6 +87,14 @@ Knobs Knobs::fromEnv() {
   return k;
 }
 
+bool useLocalSimpleFifo(bool oneGpu, const Knobs& k, const std::vector<Algorithm>& algos,
+                        const std::vector<int>& sendRun) {
+  if (!oneGpu || k.simpleBuffEnv) return false;
+  for (size_t a = 0; a < algos.size(); a++)
+    if (algos[a].proto == kProtoSimple && a < sendRun.size() && sendRun[a] > 2) return false;
+  return true;
+}
+
 int chooseSplit(int maxBlocks, int coResident, const Knobs& kn) {
   int k = 1;
   if (kn.split > 0) {
@@ -283,13 +291,31 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p) {
   return 0;
 }
 
-int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p) {
-  // Where the fold beats the interpreted schedule (co-resident ranks, graph replay,
+int64_t foldLinkCrossoverBytes(int nRanks) {
+  if (nRanks <= 2) return -1;
+  const double f = 2.0;  // LL: a 16-B line per 8-B payload
+  const double bytesPerUs = kXgmiLinkOneWayGBs * 1e3;
+  return (int64_t)((kInterpFixedUs + kXgmiHopUs) * bytesPerUs / (f * (1.0 - 2.0 / nRanks)));
+}
+
+int64_t defaultLowerMaxBytes(int nRanks, bool remote) {
+  // Ranks on one GPU, where the fold beats the interpreted schedule (graph replay,
   // profiles/r04b_xover.txt, r04l_sweep.txt): 2 ranks up to a few KiB (the exchange-set kernel
-  // runs the pair exchange itself in ~6.6 us from 8 KiB on), 8 ranks up to 128 KiB (16 fold
+  // runs the pair exchange itself in ~6.6 us from 8 KiB on), more ranks up to 128 KiB (16 fold
   // workgroups per rank, profiles/r04t_lat.txt: the one-shot 64 KiB 23.7 -> 11.3 us, the two-phase
   // all-pairs 128 KiB 17.9-21.1 -> 13.1; at 256 KiB 21.6 against 21.2, even)
-  const int64_t limit = k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : c.nRanks <= 2 ? (int64_t)(4 << 10) : (int64_t)(128 << 10);
+  if (!remote || nRanks <= 2) return nRanks <= 2 ? (int64_t)(4 << 10) : (int64_t)(128 << 10);
+  // Peers on other GPUs: the link model's crossover, rounded down to a power of two and capped at
+  // the size where the fold kernel's 16 workgroups per rank stop keeping up on one GPU.  Two
+  // ranks keep the co-resident value: the pair exchange is one hop with the fold's link bytes.
+  const int64_t x = foldLinkCrossoverBytes(nRanks);
+  int64_t p = 4 << 10;
+  while (p * 2 <= x && p * 2 <= kFoldMaxBytesCap) p *= 2;
+  return p;
+}
+
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p) {
+  const int64_t limit = k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : defaultLowerMaxBytes(c.nRanks, c.remote);
   if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > limit ||
       p->nBytes > (1ll << 30))
     return 1;
@@ -372,6 +398,72 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
     const int64_t align = (int64_t)nt * 8;
     last = (last + align - 1) / align * align;
     p->ringLastChunk = last / ts;
+  }
+  return 0;
+}
+
+int planCall(const PlanContext& ctx, const CallDesc& c, bool asyncMany, Plan* p) {
+  const std::vector<Algorithm>& algos = *ctx.algos;
+  const Knobs& k = *ctx.knobs;
+  // the ring / tree fallback, or its flat form (one hop) when the flat group exists
+  auto fallback = [&]() {
+    if (!ctx.ringFallback || makeRingPlan(c, k, p) != 0) return false;
+    if (ctx.flat) makeFlatTreePlan(c, k, p);
+    return true;
+  };
+  if (asyncMany && k.referenceSelection && c.customAlgo >= 0) {
+    WARN("MSCCL algorithms is not supposed to be used in async mode!");  // enqueue.cc:448-451
+    return 5;  // ncclInvalidUsage
+  }
+  const int idx = asyncMany && k.referenceSelection ? -1 : selectAlgo(algos, *ctx.regs, c, k);
+  if (idx < 0) {
+    // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
+    if (fallback()) {
+      INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; %s fallback (%s, %d channels)", c.coll,
+           c.count, c.dtype, p->ringColl == kTreeFlat ? "flat" : p->ringColl == kTreeAllReduce ? "tree" : "ring",
+           p->proto == kProtoLL ? "LL" : "Simple", p->ringChannels);
+      return 0;
+    }
+    WARN("MSCCL: no loaded algorithm matches coll=%d count=%zu type=%d op=%d inplace=%d nranks=%d "
+         "and the ring fallback %s", c.coll, c.count, c.dtype, c.redop, (int)c.inPlace, c.nRanks,
+         ctx.ringFallback ? "does not support it" : "is disabled (MSCCL_AMD_RING_FALLBACK=0)");
+    return 5;
+  }
+  int protoOverride = -1;
+  for (auto& r : *ctx.regs)
+    if (r.algoIndex == idx) protoOverride = r.proto;
+  if ((protoOverride >= 0 ? protoOverride : algos[idx].proto) == kProtoLL128 && c.remote && !k.ll128Remote) {
+    // The CDNA4 LL128 line relies on a 16-B store arriving untorn.  That is observed for local
+    // HBM, not shown for xGMI peer stores; the reference likewise enables LL128 only where its
+    // line atomicity holds (tuning.cc:210-214).  Run the schedule with LL (same values for the
+    // commutative ops MSCCL admits) unless MSCCL_AMD_LL128_REMOTE=1.
+    static bool warned = false;
+    if (!warned) {
+      warned = true;
+      WARN("MSCCL: algorithm %s is LL128 and peers are on other GPUs; running it with LL "
+           "(MSCCL_AMD_LL128_REMOTE=1 keeps LL128)", algos[idx].name.c_str());
+    }
+    protoOverride = kProtoLL;
+  }
+  const int r = makePlan(algos, idx, protoOverride, c, k, p);
+  if (r != 0) return r;
+  const int classes = ctx.foldClasses && (size_t)idx < ctx.foldClasses->size() ? (*ctx.foldClasses)[idx] : 0;
+  if (classes > 0 && ctx.flat && lowerToFoldPlan(c, k, classes, p) == 0) {
+    // a one-hop schedule (lower.cc): the fold kernel computes its values in one hop
+    INFO(kSubColl, "MSCCL: %s count=%zu runs as the one-hop fold", algos[idx].name.c_str(), c.count);
+    return 0;
+  }
+  if (p->scratchNeeded > ctx.scratchSize) {
+    // The scratch is sized from the XMLs' maxBytes at init (init.cc:809-835), so this only
+    // happens when MSCCL_AMD_MAX_SCRATCH capped it.  The reference reports ncclInternalError
+    // (enqueue.cc:580-589); the capped schedule is treated as not matching instead.
+    const size_t need = p->scratchNeeded;
+    if (fallback()) {
+      INFO(kSubColl, "MSCCL: scratch %zu < %zu needed (MSCCL_AMD_MAX_SCRATCH); ring fallback", ctx.scratchSize, need);
+      return 0;
+    }
+    WARN("MSCCL: MSCCL scratch pad size is smaller than expected %zu < %zu", ctx.scratchSize, need);
+    return 3;  // ncclInternalError
   }
   return 0;
 }

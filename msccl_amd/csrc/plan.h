@@ -24,6 +24,7 @@ struct CallDesc {
   int nRanks, rank;
   bool inPlace;
   int customAlgo = -1;  // ncclCustomCollective algorithm index
+  bool remote = false;  // some peer runs on another GPU (ncclComm::anyRemote): link-model defaults
 };
 
 struct Plan {
@@ -91,6 +92,11 @@ struct Knobs {
 // communicator with a Simple schedule that sends more than two chunks before it receives
 // (init.cc: applySplits).
 constexpr int64_t kLocalSimpleBuff = 256 << 10;
+// init's decision (init.cc: applySplits), the same on every rank: oneGpu = every rank of the
+// communicator on one GPU; sendRun = per algorithm the longest run of sent chunks before a
+// receive over every rank's program (algoSendRunOf)
+bool useLocalSimpleFifo(bool oneGpu, const Knobs& k, const std::vector<Algorithm>& algos,
+                        const std::vector<int>& sendRun);
 
 int refTypeSize(int dtype);
 bool inPlaceOf(int coll, const void* send, const void* recv, size_t count, int dtype, int rank);
@@ -129,5 +135,38 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p);
 // classes: the schedule's fold orders (lower.h); with several, the call's chunks must be whole
 // 16-B packs (each pack folds in its chunk's order).
 int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p);
+// What a communicator's per-call planning reads besides the call itself (enqueue.cc: planOp).
+// The introspection mscclAmdLaunchPlanJson fills the same from XML files and a placement, so
+// what it reports is what a communicator of that placement launches.
+struct PlanContext {
+  const std::vector<Algorithm>* algos = nullptr;
+  const std::vector<Registration>* regs = nullptr;
+  const Knobs* knobs = nullptr;                   // after init's agreed adjustments (FIFO sizes)
+  const std::vector<int>* foldClasses = nullptr;  // per algorithm: fold orders when lowered, else 0
+  bool flat = false;          // the flat group's connections exist (transport.cc: flatEnabled)
+  bool ringFallback = true;   // MSCCL_AMD_RING_FALLBACK
+  size_t scratchSize = 0;     // MSCCL scratch allocated at init
+};
+// One call of a communicator of more than one rank (the reference's selection, enqueue.cc:448-476
+// and 591-734): an MSCCL schedule (LL128 run as LL towards other GPUs unless allowed), the
+// lowered fold, or the ring / tree / flat fallback.  asyncMany: the group holds more than one op
+// of the communicator.  Returns an ncclResult_t code.
+int planCall(const PlanContext& ctx, const CallDesc& c, bool asyncMany, Plan* p);
+// The default of MSCCL_AMD_LOWER_MAX_BYTES:the largest call (bytes per rank) a lowered schedule
+// runs as the fold.  Ranks sharing one GPU: measured (4 KiB for 2 ranks, 128 KiB above).  Peers
+// on other GPUs: the xGMI link model below, capped at the fold kernel's own
+// throughput limit.
+int64_t defaultLowerMaxBytes(int nRanks, bool remote);
+// The link model's crossover (bytes per rank) between the fold and the two-phase all-pairs
+// schedule of n ranks, one rank per GPU: the fold sends f.S on each of its n - 1 links in one
+// hop, the two-phase schedule 2 f.S / n per link in two hops and with the interpreter's larger
+// fixed cost, so the fold wins while S < (dF + L) B / (f (1 - 2/n)).  Infinite (-1) for n <= 2,
+// where both move the same link bytes in one hop.
+int64_t foldLinkCrossoverBytes(int nRanks);
+// the model's parameters
+constexpr double kXgmiLinkOneWayGBs = 76.8;  // MI355X: 153.6 GB/s per link, both directions
+constexpr double kXgmiHopUs = 2.0;           // one cross-GPU LL hand-off (assumed until the 8-GPU sweep)
+constexpr double kInterpFixedUs = 5.0;       // interpreter over fold fixed cost (8 ranks, 128 B: 13.8 - 8.8 us)
+constexpr int64_t kFoldMaxBytesCap = 256 << 10;  // co-resident even point of the fold (16 workgroups)
 
 }  // namespace msccl

@@ -222,15 +222,16 @@ def _bench():
 
 def _c3_xml(tmp_path, nbytes):
     b = _bench()
-    tiers = b.make_xmls(8, "LL", 4, str(tmp_path))
+    tiers = b.make_xmls(8, "LL", 8, str(tmp_path), remote=True)
     return open(b.tier_of(tiers, nbytes)[3]).read()
 
 
 @needs8
-@pytest.mark.parametrize("nbytes", [128, 64 << 10, 32 << 20])
+@pytest.mark.parametrize("nbytes", [128, 64 << 10, 256 << 10, 32 << 20])
 def test_c3_init_all_eight_devices(tmp_path, nbytes):
-    """C3 (8 ranks, LL, fp16) through ncclCommInitAll(0..7) and bench.py's tier schedule of the size:
-    peer pointers over xGMI to all 7 peers, bit-exact against the oracle."""
+    """C3 (8 ranks, LL, fp16) through ncclCommInitAll(0..7) and bench.py's tier schedule of the size
+    for ranks on different GPUs: peer pointers over xGMI to all 7 peers, bit-exact against the
+    oracle (256 KiB: lowered to the fold by the link model's limit, plan.cc)."""
     from tests.gpu_harness import run_collective
     gpu, ora, _ = run_collective(_c3_xml(tmp_path, nbytes), 8, L.ALLREDUCE, nbytes // 2, 6, 0, True, seed=31,
                                  devices=list(range(8)))
@@ -263,13 +264,14 @@ def test_c5_init_all_eight_devices():
     _check(gpu, ora, "C5 AllGather on 8 devices")
 
 
-def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out):
-    """One rank of an 8-process job: every (coll, count, dt, seed) of `jobs` in place (AllReduce)
-    or out of place (RS / AG), results back to the parent."""
+def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out, one_gpu=False):
+    """One rank of a one-process-per-rank job: every (coll, count, dt, seed) of `jobs` in place
+    (AllReduce) or out of place (RS / AG), results back to the parent.  one_gpu: every process on
+    cuda:0 (hipIpc FIFOs between processes of one GPU), else rank r on cuda:r."""
     import torch
     os.environ["MSCCL_XML_FILES"] = xml_path
     os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "60"
-    torch.cuda.set_device(rank)
+    torch.cuda.set_device(0 if one_gpu else rank)
     uid = M.get_unique_id() if rank == 0 else None
     if rank == 0:
         for _ in range(world - 1):
@@ -278,9 +280,10 @@ def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out):
         uid = q_in.get(timeout=120)
     from tests.gpu_harness import gen_inputs, to_torch
     comm = M.Comm.init_rank(world, uid, rank)
-    dev = torch.device("cuda", rank)
+    dev = torch.device("cuda", 0 if one_gpu else rank)
     s = torch.cuda.current_stream().cuda_stream
     outs = []
+    kernels = []
     for coll, count, dt, seed in jobs:
         if coll == L.ALLREDUCE:
             t = to_torch(gen_inputs(world, count, dt, seed)[rank], dev)
@@ -295,14 +298,16 @@ def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out):
             comm.all_gather(x.data_ptr(), t.data_ptr(), count, dt, s)
         torch.cuda.synchronize()
         outs.append(t.cpu().numpy())
+        kernels.append(comm.info()["last"]["small"])  # 0 general, 1 small, 2 fold kernel
     err = comm.async_error()
+    remote = comm.info()["anyRemote"]
     comm.destroy()
-    q_out.put((rank, err, outs))
+    q_out.put((rank, err, outs, kernels, remote))
 
 
-def _eight_processes(tmp_path, xmls, jobs):
+def _eight_processes(tmp_path, xmls, jobs, world=8, one_gpu=False):
+    """`world` rank processes (8 by default), results {rank: (async error, outputs, kernels, anyRemote)}."""
     import torch.multiprocessing as mp
-    world = 8
     paths = []
     for i, x in enumerate(xmls):
         p = tmp_path / ("s%d.xml" % i)
@@ -310,45 +315,47 @@ def _eight_processes(tmp_path, xmls, jobs):
         paths.append(str(p))
     ctx = mp.get_context("spawn")
     q_in, q_out = ctx.Queue(), ctx.Queue()
-    ps = [ctx.Process(target=_rank_proc8, args=(r, world, ":".join(paths), jobs, q_in, q_out)) for r in range(world)]
+    ps = [ctx.Process(target=_rank_proc8, args=(r, world, ":".join(paths), jobs, q_in, q_out, one_gpu))
+          for r in range(world)]
     for pr in ps:
         pr.start()
     res = {}
     for _ in range(world):
-        r, err, outs = q_out.get(timeout=600)
-        res[r] = (err, outs)
+        r, err, outs, kernels, remote = q_out.get(timeout=600)
+        res[r] = (err, outs, kernels, remote)
     for pr in ps:
         pr.join(timeout=120)
         assert pr.exitcode == 0
     return res
 
 
-def _oracle(xmls, coll, count, dt, seed, in_place):
-    """The oracle's outputs of one call of the 8-rank job (the schedule the reference's selection
-    picks among xmls, tests/gpu_harness.py: CoResident.oracle without a GPU)."""
+def _oracle(xmls, coll, count, dt, seed, in_place, world=8):
+    """The oracle's outputs of one call of the job (the schedule the reference's selection picks
+    among xmls, tests/gpu_harness.py: CoResident.oracle without a GPU)."""
     import types
     from tests.gpu_harness import CoResident, gen_inputs
-    world = 8
     fake = types.SimpleNamespace(n=world, algos=[[L.parse_xml(x, r, world) for x in xmls] for r in range(world)])
     n_in = count * world if coll == L.REDUCE_SCATTER else count
     outs, _ = CoResident.oracle(fake, coll, count, dt, 0, gen_inputs(world, n_in, dt, seed), in_place)
     return outs
 
 
-@needs8
-def test_eight_processes_c3_c5_ipc(tmp_path):
-    """One process per GPU (the reference's mpirun -np 8 -g 1, README.md:57): hipIpc FIFOs between
-    all 8 GPUs, C3's tiers at 128 B / 64 KiB / 32 MiB, then C5's ReduceScatter and AllGather, every
-    rank bit-exact against the oracle."""
+def _c3_c5_job(tmp_path, remote):
+    """bench.py's 8-rank C3 tiers (fp16; one rank per GPU: the remote tiers) at 128 B, 64 KiB,
+    256 KiB and 32 MiB, then C5's ReduceScatter and AllGather (fp32, 64 MiB, bench.py's 8
+    instances)."""
     b = _bench()
-    tiers = b.make_xmls(8, "LL", 4, str(tmp_path))
+    tiers = b.make_xmls(8, "LL", 8, str(tmp_path), remote=remote)
     c3 = [open(t[3]).read() for t in tiers]
     rc = (64 << 20) // 4 // 8
-    c5 = [xmlgen.reduce_scatter_allpairs(8, 4, "Simple", False, 0, 1 << 40, name="c5_rs"),
-          xmlgen.allgather_allpairs(8, 4, "Simple", False, 0, 1 << 40, name="c5_ag")]
-    jobs = [(L.ALLREDUCE, nb // 2, 6, 40 + k) for k, nb in enumerate((128, 64 << 10, 32 << 20))]
+    c5 = [xmlgen.reduce_scatter_allpairs(8, 8, "Simple", False, 0, 1 << 40, name="c5_rs"),
+          xmlgen.allgather_allpairs(8, 8, "Simple", False, 0, 1 << 40, name="c5_ag")]
+    jobs = [(L.ALLREDUCE, nb // 2, 6, 40 + k) for k, nb in enumerate((128, 64 << 10, 256 << 10, 32 << 20))]
     jobs += [(L.REDUCE_SCATTER, rc, 7, 50), (L.ALLGATHER, rc, 7, 51)]
-    res = _eight_processes(tmp_path, c3 + c5, jobs)
+    return c3, c5, jobs
+
+
+def _check_c3_c5(res, c3, c5, jobs):
     for j, (coll, count, dt, seed) in enumerate(jobs):
         xs = c3 if coll == L.ALLREDUCE else c5
         want = _oracle(xs, coll, count, dt, seed, coll == L.ALLREDUCE)
@@ -358,12 +365,93 @@ def test_eight_processes_c3_c5_ipc(tmp_path):
 
 
 @needs8
+def test_eight_processes_c3_c5_ipc(tmp_path):
+    """One process per GPU (the reference's mpirun -np 8 -g 1, README.md:57): hipIpc FIFOs between
+    all 8 GPUs, C3's remote tiers (256 KiB lowered to the fold by the link model), then C5's
+    ReduceScatter and AllGather, every rank bit-exact against the oracle."""
+    c3, c5, jobs = _c3_c5_job(tmp_path, True)
+    res = _eight_processes(tmp_path, c3 + c5, jobs)
+    _check_c3_c5(res, c3, c5, jobs)
+    assert all(res[r][3] == 1 for r in range(8))
+    assert [res[0][2][j] for j in range(4)] == [2, 2, 2, 1]  # fold up to 256 KiB, then the small kernel
+
+
+def test_eight_processes_one_gpu_c3_c5_ipc(tmp_path):
+    """The driver's 8-process configuration on one GPU (bench.py --gpus 8 with
+    MSCCL_AMD_BENCH_ONE_GPU=1): 8 rank processes on cuda:0, FIFOs mapped with hipIpc between
+    processes, bench.py's 8-rank C3 tiers and C5's pair at full size, every rank bit-exact against
+    the oracle.  Runs on any box (the needs8 form above takes the same jobs across 8 GPUs)."""
+    c3, c5, jobs = _c3_c5_job(tmp_path, False)
+    res = _eight_processes(tmp_path, c3 + c5, jobs, one_gpu=True)
+    _check_c3_c5(res, c3, c5, jobs)
+    assert all(res[r][3] == 0 for r in range(8))
+    assert [res[0][2][j] for j in range(4)] == [2, 2, 1, 1]  # co-resident: fold up to 128 KiB
+
+
+def _c4_job():
+    xml = xmlgen.allreduce_ring(8, 32, "Simple", True, 0, 1 << 40, name="c4_ring")
+    return xml, [(L.ALLREDUCE, (8 << 20) // 2, 9, 60)]
+
+
+@needs8
 def test_eight_processes_c4_ipc(tmp_path):
     """C4 one rank per GPU: the 32-ring Simple bf16 schedule at 8 MiB per rank against the oracle."""
-    xml = xmlgen.allreduce_ring(8, 32, "Simple", True, 0, 1 << 40, name="c4_ring")
-    jobs = [(L.ALLREDUCE, (8 << 20) // 2, 9, 60)]
+    xml, jobs = _c4_job()
     res = _eight_processes(tmp_path, [xml], jobs)
     want = _oracle([xml], L.ALLREDUCE, (8 << 20) // 2, 9, 60, True)
     for r in range(8):
         assert res[r][0] == 0
         _check([res[r][1][0]], [want[r]], "C4 8 processes rank %d" % r)
+
+
+def test_eight_processes_one_gpu_c4_ipc(tmp_path):
+    """C4's 32-ring Simple bf16 schedule, 8 rank processes on cuda:0 (hipIpc), 8 MiB per rank,
+    bit-exact against the oracle."""
+    xml, jobs = _c4_job()
+    res = _eight_processes(tmp_path, [xml], jobs, one_gpu=True)
+    want = _oracle([xml], L.ALLREDUCE, (8 << 20) // 2, 9, 60, True)
+    for r in range(8):
+        assert res[r][0] == 0
+        _check([res[r][1][0]], [want[r]], "C4 8 processes on one GPU rank %d" % r)
+
+
+# ------------------------------------------------------------------------------------------------
+# four devices: bench.py --gpus 4 (fp32, one rank per GPU, the 4-rank remote tiers)
+
+needs4 = pytest.mark.skipif("_ndev() < 4", reason="needs four visible GPUs (bench.py --gpus 4, one rank per GPU)")
+
+
+def _four_rank_job(tmp_path, remote):
+    b = _bench()
+    tiers = b.make_xmls(4, "LL", 8, str(tmp_path), remote=remote)
+    xmls = [open(t[3]).read() for t in tiers]
+    jobs = [(L.ALLREDUCE, nb // 4, 7, 70 + k) for k, nb in enumerate((128, 64 << 10, 256 << 10, 4 << 20, 32 << 20))]
+    return xmls, jobs
+
+
+def _check_four(res, xmls, jobs):
+    for j, (coll, count, dt, seed) in enumerate(jobs):
+        want = _oracle(xmls, coll, count, dt, seed, True, world=4)
+        for r in range(4):
+            assert res[r][0] == 0
+            _check([res[r][1][j]], [want[r]], "4 processes job %d rank %d" % (j, r))
+
+
+@needs4
+def test_four_processes_four_devices_bench_tiers(tmp_path):
+    """bench.py --gpus 4: 4 rank processes on 4 GPUs (hipIpc over xGMI), the 4-rank remote tiers
+    (one-shot below 64 KiB, two-phase all-pairs above, fold up to the link model's 256 KiB), fp32,
+    128 B to 32 MiB, bit-exact against the oracle."""
+    xmls, jobs = _four_rank_job(tmp_path, True)
+    res = _eight_processes(tmp_path, xmls, jobs, world=4)
+    _check_four(res, xmls, jobs)
+    assert all(res[r][3] == 1 for r in range(4))
+    assert [res[0][2][j] for j in range(3)] == [2, 2, 2]
+
+
+def test_four_processes_one_gpu_bench_tiers(tmp_path):
+    """The same 4-rank job with the 4 processes on cuda:0 (co-resident tiers and limits)."""
+    xmls, jobs = _four_rank_job(tmp_path, False)
+    res = _eight_processes(tmp_path, xmls, jobs, world=4, one_gpu=True)
+    _check_four(res, xmls, jobs)
+    assert [res[0][2][j] for j in range(3)] == [2, 2, 1]

@@ -1,0 +1,109 @@
+"""What a communicator launches, with init's decisions, by placement (plan.cc: planCall through
+mscclAmdLaunchPlanJson; no GPU): the one-hop lowering limit from the link model for ranks on
+different GPUs against the measured co-resident limit, the local Simple FIFO, the
+trace / NPKit rule that keeps a schedule interpreted."""
+import pytest
+
+import msccl_amd as M
+from msccl_amd import xmlgen
+from oracle import loader as L
+
+
+def _files(tmp_path, xmls):
+    paths = []
+    for i, x in enumerate(xmls):
+        p = tmp_path / ("s%d.xml" % i)
+        p.write_text(x)
+        paths.append(str(p))
+    return ":".join(paths)
+
+
+def test_link_model_defaults():
+    """The remote limit is the model's crossover (dF + L) B / (f (1 - 2/n)) floored to a power of
+    two and capped at 256 KiB; co-resident ranks keep the measured 4 KiB / 128 KiB; two ranks keep
+    4 KiB (the pair exchange is already one hop with the fold's link bytes)."""
+    b_us = 76.8e3                     # one xGMI link, one way, bytes per microsecond
+    for n in (3, 4, 8, 16):
+        x = (5.0 + 2.0) * b_us / (2.0 * (1 - 2.0 / n))
+        p = 4096
+        while p * 2 <= x and p * 2 <= 256 << 10:
+            p *= 2
+        assert p == 256 << 10        # every n >= 3 reaches the cap with these parameters
+    xml = xmlgen.allreduce_allpairs(8, 1, "LL")
+    import tempfile
+    import os
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "a.xml")
+        open(path, "w").write(xml)
+        for one_gpu, want in ((True, 128 << 10), (False, 256 << 10)):
+            got = M.launch_plan_json(path, 0, 8, one_gpu, L.ALLREDUCE, 1024, 7, 0, True)
+            assert got["lowerMaxBytes"] == want, got
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "p.xml")
+        open(path, "w").write(xmlgen.allreduce_pair_oneshot(16, "LL"))
+        for one_gpu in (True, False):
+            assert M.launch_plan_json(path, 0, 2, one_gpu, L.ALLREDUCE, 1024, 7, 0, True)["lowerMaxBytes"] == 4096
+
+
+@pytest.mark.parametrize("nbytes,co,remote", [
+    (128, "fold", "fold"), (64 << 10, "fold", "fold"), (128 << 10, "fold", "fold"),
+    (256 << 10, "interpreter", "fold"), (512 << 10, "interpreter", "interpreter"),
+    (32 << 20, "interpreter", "interpreter")])
+def test_c3_tiers_by_placement(tmp_path, nbytes, co, remote):
+    """bench.py's 8-rank tiers (C3, fp16): up to 128 KiB both placements run the fold; at 256 KiB
+    only ranks on different GPUs do (the link model), above neither."""
+    import bench
+    tiers = bench.make_xmls(8, "LL", 8, str(tmp_path))
+    files = ":".join(t[3] for t in tiers)
+    for one_gpu, want in ((True, co), (False, remote)):
+        got = M.launch_plan_json(files, 3, 8, one_gpu, L.ALLREDUCE, nbytes // 2, 6, 0, True)
+        assert got["kernel"] == want, (one_gpu, got)
+        assert got["lowered"] == (want == "fold")
+        assert got["remote"] == (0 if one_gpu else 1)
+
+
+def test_lower_limit_knob_overrides_both(tmp_path, monkeypatch):
+    files = _files(tmp_path, [xmlgen.allreduce_allpairs(8, 1, "LL")])
+    monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "8192")
+    for one_gpu in (True, False):
+        got = M.launch_plan_json(files, 0, 8, one_gpu, L.ALLREDUCE, 16384 // 4, 7, 0, True)
+        assert got["lowerMaxBytes"] == 8192 and got["kernel"] == "interpreter", got
+
+
+@pytest.mark.parametrize("env", ["MSCCL_AMD_TRACE=1", "MSCCL_AMD_NPKIT=1", "MSCCL_AMD_LOWER=0"])
+def test_traced_schedule_runs_as_written(tmp_path, monkeypatch, env):
+    """A full trace or NPKit records the schedule's own primitives: no lowering."""
+    files = _files(tmp_path, [xmlgen.allreduce_allpairs(8, 1, "LL")])
+    assert M.launch_plan_json(files, 0, 8, True, L.ALLREDUCE, 1024, 7, 0, True)["kernel"] == "fold"
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    got = M.launch_plan_json(files, 0, 8, True, L.ALLREDUCE, 1024, 7, 0, True)
+    assert got["kernel"] == "interpreter" and got["classes"] == [0], got
+
+
+def test_light_trace_keeps_lowering(tmp_path, monkeypatch):
+    files = _files(tmp_path, [xmlgen.allreduce_allpairs(8, 1, "LL")])
+    monkeypatch.setenv("MSCCL_AMD_TRACE", "2")
+    assert M.launch_plan_json(files, 0, 8, True, L.ALLREDUCE, 1024, 7, 0, True)["kernel"] == "fold"
+
+
+def test_local_simple_fifo_by_placement(tmp_path, monkeypatch):
+    """256 KiB Simple FIFO only when every rank shares one GPU, NCCL_BUFFSIZE is unset and no
+    Simple schedule sends more than two chunks before it receives (init.cc: applySplits)."""
+    ring = _files(tmp_path, [xmlgen.allreduce_ring(8, 4, "Simple", True)])
+    assert M.launch_plan_json(ring, 0, 8, True, L.ALLREDUCE, 1 << 20, 9, 0, True)["simpleBuffBytes"] == 256 << 10
+    assert M.launch_plan_json(ring, 0, 8, False, L.ALLREDUCE, 1 << 20, 9, 0, True)["simpleBuffBytes"] == 4 << 20
+    monkeypatch.setenv("NCCL_BUFFSIZE", str(1 << 20))
+    assert M.launch_plan_json(ring, 0, 8, True, L.ALLREDUCE, 1 << 20, 9, 0, True)["simpleBuffBytes"] == 1 << 20
+
+
+def test_fallback_and_ll128_remote(tmp_path):
+    """No schedule matches: the flat fold (LL range) or the ring; an LL128 schedule runs as LL
+    across GPUs (the line-tear gate) and as LL128 on one GPU."""
+    files = _files(tmp_path, [xmlgen.allreduce_allpairs(4, 1, "LL128")])
+    assert M.launch_plan_json(files, 0, 4, True, L.ALLREDUCE, 1 << 14, 7, 0, True)["proto"] == 1
+    assert M.launch_plan_json(files, 0, 4, False, L.ALLREDUCE, 1 << 14, 7, 0, True)["proto"] == 0
+    got = M.launch_plan_json(files, 0, 4, False, L.ALLREDUCE, 1001, 7, 0, True)
+    assert got["kernel"] == "fold" and got["algo"] == -1, got
+    got = M.launch_plan_json(files, 0, 4, False, L.ALLREDUCE, (8 << 20) + 1, 7, 0, True)
+    assert got["kernel"] == "ring", got

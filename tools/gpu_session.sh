@@ -121,6 +121,15 @@ for c, d in json.load(open('${O}_c4k.json'))['configs'].items():
       > ${O}_spawn2.json 2> ${O}_spawn2.err || fail spawn ${O}_spawn2.err
     timeout -k 10 120 python3 bench.py --gpus 2 > ${O}_refuse2.json 2> ${O}_refuse2.err
     echo "refuse rc=$?" | tee ${O}_refuse2.rc ;;
+  rehearse)
+    # the driver's multi-GPU bench command, its N rank processes on cuda:0 (REHEARSE_N, default 8;
+    # at 8 the C4 / C5 extras run too), the default K / W
+    RN=${REHEARSE_N:-8}
+    MSCCL_AMD_BENCH_ONE_GPU=1 timeout -k 10 600 python3 bench.py --gpus $RN ${REHEARSE_ARGS} \
+      > ${O}_rehearse_$RN.json 2> ${O}_rehearse_$RN.err || fail "rehearse $RN" ${O}_rehearse_$RN.err
+    python3 -c "
+import json; d = json.load(open('${O}_rehearse_$RN.json'))
+print('rehearse $RN', d['value'], d['avg_busbw'], d['verified'], {k: {p: v[p].get('kernel_ms') if isinstance(v.get(p), dict) else v.get(p) for p in v if p in ('allreduce', 'reduce_scatter', 'all_gather', 'verified', 'error')} for k, v in d.get('configs', {}).items()})" ;;
   sweep)
     for L in $LIBS; do
       b=$(basename $L .so)
