@@ -151,3 +151,37 @@ def test_ring_lowered_per_start_class(tmp_path, inst):
         for count, dt in ((8 * inst * 64, 6), (8 * inst * 8 * 37, 9)):
             last, _ = _case(cr, count, dt, count % 53)
             assert last["small"] == 2, last
+
+
+@pytest.mark.parametrize("dt", [6, 7])
+def test_lowered_fold_nan_positions(tmp_path, monkeypatch, dt):
+    """NaN payloads are outside the fold's bit-exact claim (with two NaN operands
+    IEEE add returns one payload by operand order).  What holds: the lowered call gives a NaN
+    exactly where the interpreted schedule does, and every other element bit for bit."""
+    import torch
+    n, count = 8, 4096
+    xml = xmlgen.allreduce_allpairs(n, 1, "LL")
+    ins = gen_inputs(n, count, dt, 77)
+    bits = {6: np.uint16, 7: np.uint32}[dt]
+    quiet = {6: 0x7E00, 7: 0x7FC00000}[dt]
+    for r in range(n):
+        v = ins[r].view(bits)
+        v[r::97] = quiet | (r + 1)            # a NaN payload per rank, at positions that overlap
+        v[(3 * r) % 11::131] = quiet | 0x100 | r
+    results = {}
+    for lower in ("1", "0"):
+        monkeypatch.setenv("MSCCL_AMD_LOWER", lower)
+        with CoResident(n, [xml], str(tmp_path)) as cr:
+            t = [to_torch(x, torch.device("cuda:0")) for x in ins]
+            torch.cuda.synchronize()
+            cr.run(L.ALLREDUCE, count, dt, 0, [x.data_ptr() for x in t], [x.data_ptr() for x in t])
+            results[lower] = [from_torch(x, N.storage(dt)) for x in t]
+            assert cr.comms[0].info()["last"]["small"] == (2 if lower == "1" else 1)
+    for r in range(n):
+        a, b = results["1"][r], results["0"][r]
+        fa = a.view(np.float16 if dt == 6 else np.float32)
+        fb = b.view(np.float16 if dt == 6 else np.float32)
+        assert np.array_equal(np.isnan(fa), np.isnan(fb)), "rank %d NaN positions differ" % r
+        keep = ~np.isnan(fa)
+        assert np.array_equal(a.view(bits)[keep], b.view(bits)[keep]), "rank %d non-NaN bits differ" % r
+        assert np.isnan(fa).sum() > 0

@@ -34,7 +34,7 @@ for step in $STEPS; do
       > ${O}_suite.txt 2>&1 || fail suite ${O}_suite.txt
     tail -2 ${O}_suite.txt ;;
   lat)
-    # LATSPECS: "schedule bytes ranks instances dtype" entries separated by ';'; LATENV: extra
+    # LATSPECS: "schedule bytes ranks instances dtype [coll]" entries separated by ';'; LATENV: extra
     # environment for every run (e.g. MSCCL_AMD_LOWER=0)
     SPECS=${LATSPECS:-"pair 128 2 1 7;pair 4096 2 16 7;pair 65536 2 16 7;oneshot 128 8 4 6;oneshot 4096 8 4 6;fbtree 128 2 1 7;fbtree 128 8 1 6"}
     for L in $LIBS; do
@@ -42,7 +42,7 @@ for step in $STEPS; do
       for spec in "${SP[@]}"; do
         set -- $spec
         r=$(env $LATENV MSCCL_AMD_LIB=$L timeout -k 5 90 python3 tools/lat_one.py --iters 300 --graph --schedule $1 \
-            --bytes $2 --ranks $3 --instances $4 --dtype $5 2>&1 | grep -v amdgpu.ids) || fail "lat $L $spec"
+            --bytes $2 --ranks $3 --instances $4 --dtype $5 --coll ${6:-ar} 2>&1 | grep -v amdgpu.ids) || fail "lat $L $spec"
         echo "$(basename $L) $LATENV $r" | tee -a ${O}_lat.txt
       done
     done ;;
@@ -80,7 +80,7 @@ print('C3 32 MiB instances $i $C3ENV', s['kernel_ms'], s['busbw'], s['kernel'])"
       python3 -c "
 import json
 for c, d in json.load(open('${O}_c4k.json'))['configs'].items():
-    print('${C4RANKS:-8} ranks', c, '$e', ' '.join('%s %s ms %s' % (k, v['kernel_ms'], v['hbm_frac']) for k, v in d.items()
+    print('${C4RANKS:-8} ranks', c, '$e', ' '.join('%s %s ms %s' % (k, v['kernel_ms'], v['memside_frac']) for k, v in d.items()
           if isinstance(v, dict) and 'kernel_ms' in v), d.get('verified'), d.get('error', ''))" | tee -a ${O}_c4knobs.txt
     done ;;
   xcdpmc)
@@ -130,6 +130,29 @@ for c, d in json.load(open('${O}_c4k.json'))['configs'].items():
     python3 -c "
 import json; d = json.load(open('${O}_rehearse_$RN.json'))
 print('rehearse $RN', d['value'], d['avg_busbw'], d['verified'], {k: {p: v[p].get('kernel_ms') if isinstance(v.get(p), dict) else v.get(p) for p in v if p in ('allreduce', 'reduce_scatter', 'all_gather', 'verified', 'error')} for k, v in d.get('configs', {}).items()})" ;;
+  traces)
+    # per-transfer attribution (tools/trace_report.py --summary) of each "schedule ranks instances
+    # proto dtype bytes" in TRSPECS (';'-separated)
+    IFS=';' read -ra TS <<< "${TRSPECS:-allgather 8 8 Simple 7 67108864}"
+    for spec in "${TS[@]}"; do
+      set -- $spec
+      MSCCL_AMD_TRACE=1 timeout -k 10 300 python3 tools/trace_report.py --schedule $1 --ranks $2 --instances $3 \
+        --proto $4 --dtype $5 --bytes $6 --iters 3 --summary >> ${O}_traces.txt 2>&1 || fail "traces $spec" ${O}_traces.txt
+    done
+    cat ${O}_traces.txt ;;
+  envsweep)
+    # the C2 sweep (or BARGS' shape) under each environment of SWEEPENVS (';'-separated, "-" = none)
+    IFS=';' read -ra EV <<< "${SWEEPENVS:--}"
+    for e in "${EV[@]}"; do
+      [ "$e" = "-" ] && e=""
+      env $e timeout -k 10 300 python3 bench.py --no-cpu --pmc off --no-secondary ${BARGS} > ${O}_es.json 2>> ${O}_es.err \
+        || fail "envsweep $e" ${O}_es.err
+      python3 -c "
+import json
+d = json.load(open('${O}_es.json'))
+print('[$e] value %.1f avg %.1f |' % (d['value'], d['avg_busbw']), ' '.join('%d:%.2f' % (s['bytes'], s['ms'] * 1e3) for s in d['sweep']), d['verified'])
+" | tee -a ${O}_envsweep.txt
+    done ;;
   sweep)
     for L in $LIBS; do
       b=$(basename $L .so)

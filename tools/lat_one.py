@@ -20,7 +20,7 @@ def main():
     ap.add_argument("--iters", type=int, default=300)
     ap.add_argument("--coll", default="ar", choices=["ar", "rs", "ag"],
                     help="AllReduce, or ReduceScatter / AllGather with --bytes per rank's block "
-                         "(fallback schedules only; fbring there is the ring, fbtree the flat form)")
+                         "(agap / rsap, or the fallback: fbring there is the ring, fbtree the flat form)")
     ap.add_argument("--graph", action="store_true",
                     help="capture the launches in one hipGraph and time its replay: device time per launch "
                          "without the host's per-call cost")
@@ -29,7 +29,36 @@ def main():
     gen = {"allpairs": lambda: xmlgen.allreduce_allpairs(a.ranks, a.instances, a.proto),
            "pair": lambda: xmlgen.allreduce_pair_oneshot(a.instances, a.proto),
            "ring": lambda: xmlgen.allreduce_ring(a.ranks, a.instances, a.proto),
-           "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2)}
+           "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2),
+           # C5's pair (--coll ag / rs, --bytes a rank's block)
+           "agap": lambda: xmlgen.allgather_allpairs(a.ranks, a.instances, a.proto, False, 0, 1 << 40),
+           "rsap": lambda: xmlgen.reduce_scatter_allpairs(a.ranks, a.instances, a.proto, False, 0, 1 << 40,
+                                                          form="chain"),
+           # RCCL's shipped 8-rank all-pairs LL file, maxBytes raised (bench.py secondary_schedules)
+           "rccl32": lambda: open("/opt/rocm/share/rccl/msccl-algorithms/allreduce-allpairs-8n-ll-32tb.xml").read()
+           .replace('maxBytes="65536"', 'maxBytes="%d"' % (1 << 40))}
+    if a.schedule == "empty":
+        # the floor: a one-element torch kernel per launch, captured and replayed the same way
+        x = torch.zeros(1, device="cuda")
+        stream = torch.cuda.Stream()
+        with torch.cuda.stream(stream):
+            for _ in range(20):
+                x.add_(1)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream):
+            for _ in range(a.iters):
+                x.add_(1)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        with torch.cuda.stream(stream):
+            g.replay()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        print("empty (one-element add) kernel: %.2f us per launch (events, graph replay)"
+              % (e0.elapsed_time(e1) * 1000 / a.iters), flush=True)
+        return
     if a.schedule in ("fbring", "fbtree", "fbchain"):   # no schedule: the ring / tree fallback
         os.environ.pop("MSCCL_XML_FILES", None)
         os.environ["NCCL_ALGO"] = "Ring" if a.schedule == "fbring" else "Tree"

@@ -80,7 +80,8 @@ def main():
     ap.add_argument("--instances", type=int, default=1)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--dtype", type=int, default=7, help="ncclDataType_t: 7 fp32, 6 fp16, 9 bf16")
-    ap.add_argument("--schedule", default="allpairs", choices=["allpairs", "pair", "ring", "oneshot"])
+    ap.add_argument("--schedule", default="allpairs",
+                    choices=["allpairs", "pair", "ring", "oneshot", "allgather", "reducescatter", "rccl32"])
     ap.add_argument("--summary", action="store_true")
     a = ap.parse_args()
     import torch
@@ -89,17 +90,31 @@ def main():
     gen = {"allpairs": lambda: xmlgen.allreduce_allpairs(a.ranks, a.instances, a.proto, max_bytes=big),
            "pair": lambda: xmlgen.allreduce_pair_oneshot(a.instances, a.proto),
            "ring": lambda: xmlgen.allreduce_ring(a.ranks, a.instances, a.proto),
-           "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2)}
+           "oneshot": lambda: xmlgen.allreduce_oneshot(a.ranks, a.instances, a.proto, ordered=a.ranks > 2),
+           # C5's pair (bench.py run_extra): --bytes is the whole buffer, a rank's block is bytes / ranks
+           "allgather": lambda: xmlgen.allgather_allpairs(a.ranks, a.instances, a.proto, False, 0, big),
+           "reducescatter": lambda: xmlgen.reduce_scatter_allpairs(a.ranks, a.instances, a.proto, False, 0, big,
+                                                                   form="chain"),
+           # RCCL's shipped 8-rank all-pairs LL file, maxBytes raised (bench.py secondary_schedules)
+           "rccl32": lambda: open("/opt/rocm/share/rccl/msccl-algorithms/allreduce-allpairs-8n-ll-32tb.xml").read()
+           .replace('maxBytes="65536"', 'maxBytes="%d"' % big)}
     open(path, "w").write(gen[a.schedule]())
     os.environ["MSCCL_XML_FILES"] = path
     comms = M.Comm.init_all([0] * a.ranks)
     ts = {7: 4, 6: 2, 9: 2}[a.dtype]
     cnt = a.bytes // ts
     bufs = [torch.zeros((a.bytes + 3) // 4, device="cuda") for _ in comms]
+    outs = [torch.zeros((a.bytes + 3) // 4, device="cuda") for _ in comms]
+    blk = cnt // a.ranks
     for _ in range(a.iters):
         with M.group():
-            for c, b in zip(comms, bufs):
-                c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, 0)
+            for c, b, o in zip(comms, bufs, outs):
+                if a.schedule == "allgather":
+                    c.all_gather(b.data_ptr(), o.data_ptr(), blk, a.dtype, 0)
+                elif a.schedule == "reducescatter":
+                    c.reduce_scatter(b.data_ptr(), o.data_ptr(), blk, a.dtype, M.SUM, 0)
+                else:
+                    c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, 0)
     torch.cuda.synchronize()
     traces = [np.asarray(c.trace()) for c in comms]
     if a.summary:
