@@ -113,9 +113,18 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
                          {launchKernel<T, kSumPostDiv, pLL>, nullptr, launchKernel<T, kSumPostDiv, pSimple>}}; \
   MSCCL_SMALL(NAME, T)                                                                                     \
   OneRankFn NAME##_one = launchOneRankScale<T>;
+#ifndef MSCCL_SMALL_ONLY
 #define MSCCL_DEFINE_TABLE_FP(NAME, T)                                                                     \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T), {nullptr, nullptr, nullptr}};                                   \
   MSCCL_SMALL(NAME, T)                                                                                     \
   OneRankFn NAME##_one = launchOneRankScale<T>;
+#else
+// measurement builds of one type's small-call and fold kernels only (tools/varbuild.sh): the
+// general kernel is not compiled, calls that need it fail to launch
+#define MSCCL_DEFINE_TABLE_FP(NAME, T)                                                                     \
+  LaunchFn NAME[6][3] = {};                                                                                \
+  MSCCL_SMALL(NAME, T)                                                                                     \
+  OneRankFn NAME##_one = launchOneRankScale<T>;
+#endif
 
 }  // namespace msccl

@@ -208,7 +208,7 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
         mb = std::max(mb, (int)r.nBlocks[a]);
         run = std::max(run, (int)r.sendRun[a]);
       }
-    comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs);
+    comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs, comm->algos[a].proto);
     comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
   }

@@ -72,7 +72,7 @@ Knobs Knobs::fromEnv() {
   k.simpleBuffEnv = getenv("NCCL_BUFFSIZE") != nullptr;
   k.ringChannels = (int32_t)envInt("MSCCL_AMD_RING_CHANNELS", 0);
   k.split = (int32_t)envInt("MSCCL_AMD_SPLIT", 0);
-  k.targetWgs = (int32_t)envInt("MSCCL_AMD_TARGET_WGS", 512);
+  k.targetWgs = (int32_t)envInt("MSCCL_AMD_TARGET_WGS", 0);  // 0: by protocol (chooseSplit)
   k.merge = (int32_t)envInt("MSCCL_AMD_MERGE", 0);
   k.ringFallback = envInt("MSCCL_AMD_RING_FALLBACK", 1) != 0;
   k.ll128Remote = envInt("MSCCL_AMD_LL128_REMOTE", 0) != 0;
@@ -95,13 +95,17 @@ bool useLocalSimpleFifo(bool oneGpu, const Knobs& k, const std::vector<Algorithm
   return true;
 }
 
-int chooseSplit(int maxBlocks, int coResident, const Knobs& kn) {
+int chooseSplit(int maxBlocks, int coResident, const Knobs& kn, int proto) {
   int k = 1;
   if (kn.split > 0) {
     while (k * 2 <= kMaxSplit && k * 2 <= kn.split) k *= 2;
     return k;
   }
-  const int64_t target = kn.targetWgs;
+  // Workgroups per GPU: one per CU for LL / LL128 schedules, two for Simple.  Same box, alternating
+  // runs (profiles/r05g_target_wgs.txt): 8 co-resident ranks, LL fp16 all-pairs 2 MiB 48.0 ->
+  // 41.8 us, 32 MiB 541 -> 532, RCCL's 8n-32tb file 602 -> 554 us (split 2 -> 1); the Simple C4
+  // ring 1.49 ms at 512 against 1.76 at 256 (r05e_c4knobs.txt)
+  const int64_t target = kn.targetWgs > 0 ? kn.targetWgs : proto == kProtoSimple ? 512 : 256;
   int64_t per = (int64_t)std::max(1, maxBlocks) * std::max(1, coResident);
   while (k * 2 <= kMaxSplit && per * k * 2 <= target) k *= 2;
   return k;

@@ -66,7 +66,7 @@ struct Knobs {
   int64_t buffSizes[3];      // NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE / NCCL_BUFFSIZE (init.cc:455-472)
   int32_t ringChannels;      // MSCCL_AMD_RING_CHANNELS (0 = auto)
   int32_t split;             // MSCCL_AMD_SPLIT (0 = auto)
-  int32_t targetWgs;         // MSCCL_AMD_TARGET_WGS
+  int32_t targetWgs;         // MSCCL_AMD_TARGET_WGS (0: by protocol, chooseSplit)
   int32_t merge;             // MSCCL_AMD_MERGE (0 = as many as fit)
   int32_t ringFallback;      // MSCCL_AMD_RING_FALLBACK
   int32_t ll128Remote;       // MSCCL_AMD_LL128_REMOTE: allow LL128 towards peers on other GPUs
@@ -106,11 +106,12 @@ int selectAlgo(const std::vector<Algorithm>& algos, const std::vector<Registrati
 // Fills *p; returns an ncclResult_t code.
 int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverride, const CallDesc& c, const Knobs& k,
              Plan* p);
-// Workgroups per XML thread block for an algorithm whose largest rank program has maxBlocks
-// thread blocks when coResident ranks share a GPU: the largest power of two <= kMaxSplit that
-// keeps the GPU's workgroups within MSCCL_AMD_TARGET_WGS (default 256 = one per CU).
-// MSCCL_AMD_SPLIT forces a value.  Every rank must compute the same value.
-int chooseSplit(int maxBlocks, int coResident, const Knobs& k);
+// Workgroups per XML thread block for an algorithm (protocol proto) whose largest rank program
+// has maxBlocks thread blocks when coResident ranks share a GPU: the largest power of two <=
+// kMaxSplit that keeps the GPU's workgroups within MSCCL_AMD_TARGET_WGS (default by protocol: 256
+// = one per CU for LL / LL128, 512 for Simple).  MSCCL_AMD_SPLIT forces a value.  Every rank must
+// compute the same value.
+int chooseSplit(int maxBlocks, int coResident, const Knobs& k, int proto);
 // The reference's fallback when no MSCCL algorithm matches (enqueue.cc:461-476): a ring
 // AllReduce / ReduceScatter / AllGather (collectives/device/all_reduce.h:14-100,
 // reduce_scatter.h:13-67, all_gather.h:13-78).  Fills *p (algoIndex -1, ringColl set) and returns

@@ -137,7 +137,7 @@ print('rehearse $RN', d['value'], d['avg_busbw'], d['verified'], {k: {p: v[p].ge
     for spec in "${TS[@]}"; do
       set -- $spec
       MSCCL_AMD_TRACE=1 timeout -k 10 300 python3 tools/trace_report.py --schedule $1 --ranks $2 --instances $3 \
-        --proto $4 --dtype $5 --bytes $6 --iters 3 --summary >> ${O}_traces.txt 2>&1 || fail "traces $spec" ${O}_traces.txt
+        --proto $4 --dtype $5 --bytes $6 --iters 3 ${TRMODE:---summary} >> ${O}_traces.txt 2>&1 || fail "traces $spec" ${O}_traces.txt
     done
     cat ${O}_traces.txt ;;
   envsweep)
@@ -145,12 +145,13 @@ print('rehearse $RN', d['value'], d['avg_busbw'], d['verified'], {k: {p: v[p].ge
     IFS=';' read -ra EV <<< "${SWEEPENVS:--}"
     for e in "${EV[@]}"; do
       [ "$e" = "-" ] && e=""
-      env $e timeout -k 10 300 python3 bench.py --no-cpu --pmc off --no-secondary ${BARGS} > ${O}_es.json 2>> ${O}_es.err \
+      env $e timeout -k 10 300 python3 bench.py --no-cpu --pmc off ${ES_SEC:---no-secondary} ${BARGS} > ${O}_es.json 2>> ${O}_es.err \
         || fail "envsweep $e" ${O}_es.err
       python3 -c "
 import json
 d = json.load(open('${O}_es.json'))
-print('[$e] value %.1f avg %.1f |' % (d['value'], d['avg_busbw']), ' '.join('%d:%.2f' % (s['bytes'], s['ms'] * 1e3) for s in d['sweep']), d['verified'])
+print('[$e] value %.1f avg %.1f |' % (d['value'], d['avg_busbw']), ' '.join('%d:%.2f' % (s['bytes'], s['ms'] * 1e3) for s in d['sweep']), d['verified'],
+      ' '.join('%s %.1f us' % (k, v.get('kernel_ms', 0) * 1e3) for k, v in d.get('schedules', {}).items()))
 " | tee -a ${O}_envsweep.txt
     done ;;
   sweep)

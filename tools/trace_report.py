@@ -72,6 +72,47 @@ def summarize(traces):
     return out
 
 
+def by_tb(traces, max_split):
+    """Per thread block (slot // maxSplit), mean over its workgroups and ranks: time in primitive
+    calls, time outside them (dependency waits, flag publishes, setup), and when it ended (us from
+    the earliest start): which thread blocks the launch waits for."""
+    t0 = min(int(tr[s, 0]["ts"]) for tr in traces for s in range(tr.shape[0]) if tr[s, 0]["type"] == 0xFFFF)
+    rows = {}
+    for tr in traces:
+        for s in range(tr.shape[0]):
+            h = tr[s, 0]
+            if h["type"] != 0xFFFF:
+                continue
+            start = prev = int(h["ts"])
+            calls = 0
+            types = []
+            begin = None
+            end = prev
+            for e in tr[s, 1:int(h["step"])]:
+                name = M.TRACE_TYPES.get(int(e["type"]), "?")
+                ts = int(e["ts"])
+                if name == "begin":
+                    begin = ts
+                    t = TT.get(int(e["arg"]) >> 24, "?")
+                    if not types or types[-1] != t:
+                        types.append(t)
+                elif name == "end" and begin is not None:
+                    calls += ts - begin
+                    begin = None
+                end = ts
+            r = rows.setdefault(s // max_split, {"calls": [], "other": [], "end": [], "types": types})
+            r["calls"].append(calls / 100.0)
+            r["other"].append((end - start - calls) / 100.0)
+            r["end"].append((end - t0) / 100.0)
+    out = []
+    for tb in sorted(rows):
+        r = rows[tb]
+        out.append("tb %3d %-28s calls %8.1f us  outside calls %8.1f  end %8.1f (max %8.1f)  [%d wgs]"
+                   % (tb, ",".join(r["types"][:6]), np.mean(r["calls"]), np.mean(r["other"]), np.mean(r["end"]),
+                      max(r["end"]), len(r["end"])))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bytes", type=int, default=128)
@@ -83,6 +124,7 @@ def main():
     ap.add_argument("--schedule", default="allpairs",
                     choices=["allpairs", "pair", "ring", "oneshot", "allgather", "reducescatter", "rccl32"])
     ap.add_argument("--summary", action="store_true")
+    ap.add_argument("--by-tb", action="store_true", help="per thread block: busy, outside calls, end")
     a = ap.parse_args()
     import torch
     path = "/tmp/trace_ap_%d.xml" % os.getpid()
@@ -117,7 +159,12 @@ def main():
                     c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, a.dtype, M.SUM, 0)
     torch.cuda.synchronize()
     traces = [np.asarray(c.trace()) for c in comms]
-    if a.summary:
+    if a.by_tb:
+        print("%s x%d, %d ranks, %d B per rank, %s, dtype %d, per thread block:" % (
+            a.schedule, a.instances, a.ranks, a.bytes, a.proto, a.dtype))
+        for line in by_tb(traces, comms[0].info()["maxSplit"]):
+            print(line)
+    elif a.summary:
         print("%s x%d, %d ranks, %d B per rank, %s, dtype %d:" % (a.schedule, a.instances, a.ranks, a.bytes,
                                                                  a.proto, a.dtype))
         for line in summarize(traces):
