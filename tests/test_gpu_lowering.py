@@ -184,4 +184,6 @@ def test_lowered_fold_nan_positions(tmp_path, monkeypatch, dt):
         assert np.array_equal(np.isnan(fa), np.isnan(fb)), "rank %d NaN positions differ" % r
         keep = ~np.isnan(fa)
         assert np.array_equal(a.view(bits)[keep], b.view(bits)[keep]), "rank %d non-NaN bits differ" % r
-        assert np.isnan(fa).sum() > 0
+        # fp32 keeps NaN; the fp16 sum clamps it to -65504 (numerics: the reference's __hadd with
+        # the clamp), so there the check is that both forms clamp the same elements
+        assert np.isnan(fa).sum() > 0 if dt == 7 else (fa == -65504).sum() > 0
