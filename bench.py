@@ -654,8 +654,10 @@ def main():
     inst = a.instances or (16 if n <= 2 else 8 if n <= 8 else max(1, 512 // (n * (n - 1))))
     sizes = [int(s) for s in a.sizes.split(",")] if a.sizes else SIZES
     tmp = os.environ.get("TMPDIR", "/tmp")
-    # peers on other GPUs: one rank per process and GPU (not the one-GPU rehearsal)
-    remote = mode == "rank" and os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") != "1"
+    # peers on other GPUs: one rank per process and GPU (not the one-GPU rehearsal, unless it forces
+    # the runtime's cross-GPU paths with MSCCL_AMD_FORCE_REMOTE=1: then the driver's 8-GPU tiers too)
+    remote = mode == "rank" and (os.environ.get("MSCCL_AMD_BENCH_ONE_GPU") != "1" or
+                                 os.environ.get("MSCCL_AMD_FORCE_REMOTE") == "1")
     tiers = make_xmls(n, a.proto, inst, tmp, a.tiers, remote=remote)
     os.environ["MSCCL_XML_FILES"] = ":".join(t[3] for t in tiers)
     os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "30")

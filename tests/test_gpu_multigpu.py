@@ -264,13 +264,14 @@ def test_c5_init_all_eight_devices():
     _check(gpu, ora, "C5 AllGather on 8 devices")
 
 
-def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out, one_gpu=False):
+def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out, one_gpu=False, env=None):
     """One rank of a one-process-per-rank job: every (coll, count, dt, seed) of `jobs` in place
     (AllReduce) or out of place (RS / AG), results back to the parent.  one_gpu: every process on
     cuda:0 (hipIpc FIFOs between processes of one GPU), else rank r on cuda:r."""
     import torch
     os.environ["MSCCL_XML_FILES"] = xml_path
     os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "60"
+    os.environ.update(env or {})
     torch.cuda.set_device(0 if one_gpu else rank)
     uid = M.get_unique_id() if rank == 0 else None
     if rank == 0:
@@ -305,7 +306,7 @@ def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out, one_gpu=False):
     q_out.put((rank, err, outs, kernels, remote))
 
 
-def _eight_processes(tmp_path, xmls, jobs, world=8, one_gpu=False):
+def _eight_processes(tmp_path, xmls, jobs, world=8, one_gpu=False, env=None):
     """`world` rank processes (8 by default), results {rank: (async error, outputs, kernels, anyRemote)}."""
     import torch.multiprocessing as mp
     paths = []
@@ -315,7 +316,7 @@ def _eight_processes(tmp_path, xmls, jobs, world=8, one_gpu=False):
         paths.append(str(p))
     ctx = mp.get_context("spawn")
     q_in, q_out = ctx.Queue(), ctx.Queue()
-    ps = [ctx.Process(target=_rank_proc8, args=(r, world, ":".join(paths), jobs, q_in, q_out, one_gpu))
+    ps = [ctx.Process(target=_rank_proc8, args=(r, world, ":".join(paths), jobs, q_in, q_out, one_gpu, env))
           for r in range(world)]
     for pr in ps:
         pr.start()
@@ -386,6 +387,19 @@ def test_eight_processes_one_gpu_c3_c5_ipc(tmp_path):
     _check_c3_c5(res, c3, c5, jobs)
     assert all(res[r][3] == 0 for r in range(8))
     assert [res[0][2][j] for j in range(4)] == [2, 2, 1, 1]  # co-resident: fold up to 128 KiB
+
+
+def test_eight_processes_one_gpu_forced_remote(tmp_path):
+    """The driver's 8-GPU configuration as closely as one GPU allows: 8 rank processes, bench.py's
+    cross-GPU tiers (8 all-pairs instances from 64 KiB, the fold up to the link model's 256 KiB)
+    and the runtime's cross-GPU paths (MSCCL_AMD_FORCE_REMOTE=1: every peer treated as remote, so
+    the system-scope Simple release / acquire, LL128 as LL, the remote lowering limit), C3's sizes
+    and C5's pair, every rank bit-exact against the oracle."""
+    c3, c5, jobs = _c3_c5_job(tmp_path, True)
+    res = _eight_processes(tmp_path, c3 + c5, jobs, one_gpu=True, env={"MSCCL_AMD_FORCE_REMOTE": "1"})
+    _check_c3_c5(res, c3, c5, jobs)
+    assert all(res[r][3] == 1 for r in range(8))
+    assert [res[0][2][j] for j in range(4)] == [2, 2, 2, 1]  # the remote limit: the fold at 256 KiB
 
 
 def _c4_job():
