@@ -1715,6 +1715,19 @@ struct Interp {
     const int64_t maxOp = w.maxOpElems;
     const uint32_t Qc = ((uint32_t)nelem + PE - 1) / PE;
     const int q0 = (int)((Qc * (uint32_t)sub) >> lg), q1 = (int)((Qc * (uint32_t)(sub + 1)) >> lg);
+    // One iteration of the ring fallback (enqueue.cc: smallEligible; sizePerChunk 0, so `whole`):
+    // run()'s ring arithmetic at grid 0 in 32 bits: runRing's realChunkSize (all_reduce.h:43-48;
+    // reduce_scatter.h / all_gather.h: lastChunkSize once the loop covers the rest), offsets from the
+    // program's chunk (AllReduce) or rank (ReduceScatter / AllGather) indices, nelem = min(real,
+    // size - offset), one workgroup per channel.  Every transfer has count 1 (maxAllowedCount 1).
+    const int ringColl = SET == kSetAll ? (int)w.ringColl : 0;
+    int ringReal = 0;
+    if (ringColl == kRingAllReduce) {
+      const int unit = w.nBlocks * (int)w.ringRanks * (int)w.minChunk;
+      ringReal = min(chunk, ((int)w.ringSize + unit - 1) / unit * (int)w.minChunk);
+    } else if (ringColl != 0) {
+      ringReal = (int)w.ringSize < w.nBlocks * chunk ? (int)w.ringLastChunk : chunk;
+    }
     // one pass: grid = offset of the pass, iter = its index; false when a transfer ends the tb
     auto runPass = [&](int grid, int iter) __attribute__((always_inline)) -> bool {
       int step = 0;
@@ -1739,7 +1752,22 @@ struct Interp {
         for (int c = 0; c < t.count; c += macT) {
           const int thisCount = macT < t.count - c ? macT : t.count - c;
           Shape s;
+          int so = grid + (t.srcoff + c) * sizePer, dso = grid + (td.dstoff + c) * sizePer;
           s.n = nelem * thisCount;
+          if (ringColl != 0) {
+            int lim;
+            if (ringColl == kRingAllReduce) {
+              so = ((t.srcoff >= 0 ? t.srcoff : t.dstoff) * w.nBlocks + bid) * ringReal;
+              dso = so;
+              lim = so;
+            } else {
+              lim = bid * ringReal;
+              so = lim + (t.srcoff >= 0 ? t.srcoff * (int)w.ringSize : 0);
+              dso = lim + (t.dstoff >= 0 ? t.dstoff * (int)w.ringSize : 0);
+            }
+            const int ne = min(ringReal, (int)w.ringSize - lim);
+            s.n = ne > 0 ? ne : 0;
+          }
           if (split == 1) {
             s.Q = (s.n + PE - 1) / PE;
             s.q0 = 0;
@@ -1751,9 +1779,7 @@ struct Interp {
             s.Lq = q1 - q0;
             s.npk = thisCount * s.Lq;
           }
-          if (!exec<true, SET>(t, srcP, dstP, grid + (t.srcoff + c) * sizePer, grid + (td.dstoff + c) * sizePer,
-                    grid + c * sizePer, sizePer, s))
-            return false;
+          if (!exec<true, SET>(t, srcP, dstP, so, dso, grid + c * sizePer, sizePer, s)) return false;
           if (t.type == tRe && c == 0) step += t.numReds - 1;
         }
         if (fused || sendCpy) {

@@ -290,9 +290,21 @@ bool smallEligible(const Planned& p, const RankWork& w) {
   const int64_t k = cs > 0 ? sp / cs : 0, m = std::min<int64_t>(std::max<int>(1, w.merge), std::max<int64_t>(1, k));
   const bool onePass = sp <= cs || (cs > 0 && sp % cs == 0 && k % m == 0);
   const bool flat = p.plan.ringColl == kTreeFlat;
-  if (!comm->knobs.smallKernel || !(p.plan.ringColl == 0 || flat) || p.plan.proto != kProtoLL || p.op.devOp > 3 ||
-      !onePass || !(w.trace == nullptr || comm->traceLight) || w.npkit != nullptr || (w.split & (w.split - 1)) != 0)
+  // the ring fallback's one-iteration calls (interpreter.h: runSmall's ring pass): runRing's loop
+  // covers the call once (AllReduce: nChannels * nRanks * chunkSize, ReduceScatter / AllGather:
+  // nChannels * chunkSize elements), every offset within 32 bits
+  const bool ring = p.plan.ringColl == kRingAllReduce || p.plan.ringColl == kRingReduceScatter ||
+                    p.plan.ringColl == kRingAllGather;
+  if (ring) {
+    const int64_t loop = (int64_t)w.nBlocks * cs * (p.plan.ringColl == kRingAllReduce ? w.ringRanks : 1);
+    const int64_t span = (int64_t)w.ringRanks * w.ringSize * refTypeSize(p.plan.dtype);
+    if (cs <= 0 || w.ringSize > loop || span > (1ll << 30) || w.split != 1) return false;
+  }
+  if (!comm->knobs.smallKernel || !(p.plan.ringColl == 0 || flat || ring) || p.plan.proto != kProtoLL ||
+      p.op.devOp > 3 || !onePass || !(w.trace == nullptr || comm->traceLight) || w.npkit != nullptr ||
+      (w.split & (w.split - 1)) != 0)
     return false;
+  if (ring) return true;
   // (ring / tree plans have no algorithm: algoIndex -1 is only read past the checks above)
   const int64_t chunks = flat ? 1 : maxChunkIndex(comm->algos[p.plan.algoIndex], p.plan.nchunksPerLoop);
   return p.plan.sizePerChunk * chunks * refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit offsets

@@ -360,3 +360,26 @@ def test_flat_tree_across_processes(monkeypatch):
     for r in range(world):
         assert res[r][0] == 0 and res[r][1] == 5 and res[r][2] == 2, res[r][:3]
         assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
+
+
+@pytest.mark.parametrize("n,coll,count,dt,in_place", [
+    (8, L.ALLREDUCE, (512 << 10) // 2, 6, True), (8, L.ALLREDUCE, 2049, 9, False), (3, L.ALLREDUCE, 4099, 7, True),
+    (8, L.REDUCE_SCATTER, 4097, 7, False), (4, L.REDUCE_SCATTER, 333, 7, True),
+    (8, L.ALLGATHER, 40001, 6, False), (2, L.ALLGATHER, 333, 6, True)])
+def test_ring_one_iteration_small_kernel(monkeypatch, n, coll, count, dt, in_place):
+    """LL ring calls whose runRing loop covers the call once run mscclSmallKernel's ring pass
+    (enqueue.cc: smallEligible, profiles/r05p_ring_small_ab.txt: 8 ranks 512 KiB 72.4 -> 62.6 us),
+    bit-exact against oracle/ring.py; MSCCL_AMD_SMALL_KERNEL=0 keeps the general kernel, same bits."""
+    monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")   # the ring itself, not its one-hop flat form
+    rp = check(n, coll, count, dt, in_place=in_place, seed=count % 17)
+    assert rp["last"]["ringColl"] in (1, 2, 3) and rp["last"]["proto"] == 0 and rp["last"]["small"] == 1, rp
+    monkeypatch.setenv("MSCCL_AMD_SMALL_KERNEL", "0")
+    rp = check(n, coll, count, dt, in_place=in_place, seed=count % 17)
+    assert rp["last"]["small"] == 0, rp
+
+
+def test_ring_multi_iteration_keeps_general_kernel(monkeypatch):
+    """A call the ring loop covers more than once stays in the general kernel."""
+    monkeypatch.setenv("MSCCL_AMD_TREE_FLAT", "0")
+    rp = check(2, L.ALLREDUCE, (512 << 10) // 2, 6)
+    assert rp["last"]["small"] == 0 and rp["last"]["proto"] == 0, rp
