@@ -365,7 +365,7 @@ def test_flat_tree_across_processes(monkeypatch):
 @pytest.mark.parametrize("n,coll,count,dt,in_place", [
     (8, L.ALLREDUCE, (512 << 10) // 2, 6, True), (8, L.ALLREDUCE, 2049, 9, False), (3, L.ALLREDUCE, 4099, 7, True),
     (8, L.REDUCE_SCATTER, 4097, 7, False), (4, L.REDUCE_SCATTER, 333, 7, True),
-    (8, L.ALLGATHER, 40001, 6, False), (2, L.ALLGATHER, 333, 6, True)])
+    (8, L.ALLGATHER, 8001, 6, False), (2, L.ALLGATHER, 333, 6, True)])
 def test_ring_one_iteration_small_kernel(monkeypatch, n, coll, count, dt, in_place):
     """LL ring calls whose runRing loop covers the call once run mscclSmallKernel's ring pass
     (enqueue.cc: smallEligible, profiles/r05p_ring_small_ab.txt: 8 ranks 512 KiB 72.4 -> 62.6 us),
