@@ -101,6 +101,10 @@ struct Interp {
   static constexpr int TS = sizeof(T);
   static constexpr int PE = 16 / TS;  // elements per 16-B pack
   static constexpr int U = 4;         // packs per lane per pass (memory-level parallelism)
+#ifndef MSCCL_SIMPLE_COPY_U
+#define MSCCL_SIMPLE_COPY_U 4
+#endif
+  static constexpr int kSimpleCopyU = MSCCL_SIMPLE_COPY_U;  // Simple copies (simpleOp): packs per lane per pass
 
   BlockShared* sh;
   DevComm* comm;
@@ -841,12 +845,15 @@ struct Interp {
       __syncthreads();
       if (RECV) rrs = makeRsrc(rc->simple + (recvStep % kFifoSteps) * (uint64_t)slotBytes);
       if (SEND) frs = makeRsrc(sc->simple + (sendStep % kFifoSteps) * (uint64_t)slotBytes);
-      for (int base = s0 + tid; base < s1; base += kNT * U) {
-        int B[U];
-        bool act[U];
-        u32x4 v[U], peer[U];
+      // packs per lane per pass: copies (one source: the FIFO or the input) keep UC in flight,
+      // reductions (both) U
+      constexpr int UU = RECV && SRC ? U : kSimpleCopyU;
+      for (int base = s0 + tid; base < s1; base += kNT * UU) {
+        int B[UU];
+        bool act[UU];
+        u32x4 v[UU], peer[UU];
 #pragma unroll
-        for (int u = 0; u < U; u++) {
+        for (int u = 0; u < UU; u++) {
           const int p = base + u * kNT;
           act[u] = p < s1;
           B[u] = act[u] ? s.bufPack(p) : 0;
@@ -854,26 +861,26 @@ struct Interp {
         }
         if (SRC) {
 #pragma unroll
-          for (int u = 0; u < U; u++)
+          for (int u = 0; u < UU; u++)
             if (act[u]) v[u] = loadPack(srs, vec, B[u], s.n);
           if constexpr (PP::kPre) {  // PreOpN = 1: the local input (prims_simple.h:209-211)
 #pragma unroll
-            for (int u = 0; u < U; u++) v[u] = PP::pre(v[u], redArg);
+            for (int u = 0; u < UU; u++) v[u] = PP::pre(v[u], redArg);
           }
         }
         if (RECV) {
 #pragma unroll
-          for (int u = 0; u < U; u++)
+          for (int u = 0; u < UU; u++)
             if (act[u]) peer[u] = ld16<kAuxFifo>(rrs, (uint32_t)(base + u * kNT - s0) * 16);
 #pragma unroll
-          for (int u = 0; u < U; u++) v[u] = SRC ? F::pack(v[u], peer[u]) : peer[u];
+          for (int u = 0; u < UU; u++) v[u] = SRC ? F::pack(v[u], peer[u]) : peer[u];
           if constexpr (PP::kPost && SRC && DST) {
 #pragma unroll
-            for (int u = 0; u < U; u++) v[u] = PP::post(v[u], redArg);
+            for (int u = 0; u < UU; u++) v[u] = PP::post(v[u], redArg);
           }
         }
 #pragma unroll
-        for (int u = 0; u < U; u++) {
+        for (int u = 0; u < UU; u++) {
           if (!act[u]) continue;
           if (SEND) st16<kAuxFifo>(frs, (uint32_t)(base + u * kNT - s0) * 16, v[u]);
           if (DST) storePack(drs, vec, B[u], s.n, v[u]);
