@@ -1699,6 +1699,11 @@ struct Interp {
     const int split = w.split;
     const int lg = __builtin_ctz((unsigned)split);
     const int bid = local >> lg, sub = local & (split - 1);
+    // the prologue's kernel arguments in the entry batch (the compiler otherwise issues the image
+    // pointer's load inside the image lanes' branch, after the first wait): 2 ranks, graph replay,
+    // same box, 3 alternating runs (profiles/r05r_pin_ab.txt): 8 KiB 6.57 -> 6.43 us, 1 MiB 7.89 ->
+    // 7.76, 4 MiB 13.02 -> 12.80
+    pinArgs(w.images, w.tbStride, w.send, w.recv, w.epochs, w.connSplit, w.maxSplit, w.comm);
     DevTbHeader hd;
     const uint64_t workIndex = prologue(w, bid, sub, hd);
 #ifndef MSCCL_LAT_TRACE
