@@ -814,6 +814,7 @@ def main():
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
                         "payload_bytes_per_rank": payload, "verified": ok, "small": small,
                         "kernel": ("mscclFoldKernel (lowered)" if lowered else
+                                   "mscclPairKernel" if last.get("pair") == 1 else
                                    "mscclSmallKernel%s" % ("<exchange set>" if last.get("set") == 1 else "")
                                    if small else "mscclKernel"),
                         "fused": bool(fz), "tier": tier[4],

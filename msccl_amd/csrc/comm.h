@@ -79,6 +79,12 @@ struct ncclComm {
   };
   std::vector<FoldProgram> algoFold;
   std::vector<int> algoSet;  // per algorithm: the small kernel's transfer set (transport.cc: algoUpload)
+  // per algorithm: thread block b's program is one fused exchange of input chunk src + b * stride
+  // into chunk dst + b * stride of buffer dstBuf (the pair kernel, RankWork::pairSrc); src -1: not
+  struct PairForm {
+    int src = -1, dst = 0, stride = 0, dstBuf = 0;
+  };
+  std::vector<PairForm> algoPair;
   std::vector<msccl::DevAlgoHost> foldAlgos;
   msccl::DevAlgoHost ringAlgos[6];  // ring fallback programs, [4] = tree, [5] = flat tree (transport.cc: ringUpload)
   msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank
@@ -143,6 +149,7 @@ struct ncclComm {
   struct LastLaunch {
     int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0, small = 0;
     int set = 0;  // the small kernel's transfer set (devcomm.h: kSetAll / kSetExchange)
+    int pair = 0;  // the exchange ran in the pair kernel (mscclPairKernel)
   } last;
 
   // user reduction ops (ncclRedOpCreatePreMulSum, enqueue.cc:1529-1580): a free list as in the

@@ -219,7 +219,7 @@ int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
   const auto& L = comm->last;
   o << "],\"last\":{\"algo\":" << L.algo << ",\"proto\":" << L.proto << ",\"split\":" << L.split
     << ",\"merge\":" << L.merge << ",\"ringColl\":" << L.ringColl << ",\"ringChannels\":" << L.ringChannels
-    << ",\"blocks\":" << L.blocks << ",\"small\":" << L.small << ",\"set\":" << L.set << "}}";
+    << ",\"blocks\":" << L.blocks << ",\"small\":" << L.small << ",\"set\":" << L.set << ",\"pair\":" << L.pair << "}}";
   return putOut(o.str(), out, outLen);
 }
 

@@ -204,6 +204,11 @@ struct RankWork {
   uint8_t merge;                // full interpreter iterations run as one (same per-element operations)
   uint8_t foldPeers;            // flat tree (mscclFoldKernel): peers, on the records of thread blocks 1..foldPeers
   int16_t epochSlots;           // the schedule's flag / epoch slots (flags and epochs point at its range)
+  // the pair kernel (mscclPairKernel; transport.cc: algoUpload's pair form): thread block b runs
+  // one fused exchange of input chunk pairSrc + b * pairStride into chunk pairDst + b * pairStride
+  // of buffer pairDstBuf (0 input, 1 output); pairSrc -1: the schedule is not of that form
+  int16_t pairSrc, pairDst, pairStride;
+  uint8_t pairDstBuf;
   int64_t maxOpElems;           // largest run of sends before a receive (elements, all sub-connections)
   // ring fallback (kRingNone for MSCCL schedules): the program's offsets are chunk / rank indices
   // of the reference's runRing (all_reduce.h:14-100, reduce_scatter.h:13-67, all_gather.h:13-78)
@@ -242,6 +247,7 @@ constexpr int kCompactLaunchRanks = 2;
 // 2-rank pair exchange, xmlgen.allreduce_pair_oneshot; enqueue.cc picks it per launch).
 enum : int { kSetAll = 0, kSetExchange = 1 };
 
+
 // Error codes in DevComm::errWord
 enum : uint32_t { kDevOk = 0, kDevTimeout = 1, kDevAbort = 2, kDevBadOp = 3 };
 
@@ -253,6 +259,10 @@ constexpr int kQueryResidency = -1;  // LaunchFn(args, kQueryResidency, _) = res
 LaunchFn getLaunchFn(int dtype, int redop, int proto);
 LaunchFn getSmallLaunchFn(int dtype, int redop, int set);  // mscclSmallKernel (LL, Sum..Min, kSet*), or null
 LaunchFn getFoldLaunchFn(int dtype, int redop);   // mscclFoldKernel (the flat tree), or null
+// The pair kernel (mscclPairKernel): a launch whose every rank runs a pair-form schedule (every
+// thread block: one fused s + rrc of one chunk at an affine chunk index, no dependency) in one
+// pass: no program image, the first FIFO step's source loaded with the connection records.
+LaunchFn getPairLaunchFn(int dtype, int redop);
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):
 // NPKit's host/GPU clock calibration.  Returns 0 on a successful launch.
 int launchClockProbe(uint64_t* hostWord, void* stream);

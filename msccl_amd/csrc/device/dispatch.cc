@@ -2,7 +2,8 @@
 #include "devcomm.h"
 
 namespace msccl {
-#define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[2][4]; extern LaunchFn N##_fold[4]; extern OneRankFn N##_one;
+#define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[2][4]; extern LaunchFn N##_fold[4]; \
+  extern LaunchFn N##_pair[4]; extern OneRankFn N##_one;
 MSCCL_DECL(gLaunch_i8)
 MSCCL_DECL(gLaunch_u8)
 MSCCL_DECL(gLaunch_i32)
@@ -36,6 +37,14 @@ LaunchFn getSmallLaunchFn(int dtype, int devOp, int set) {
 LaunchFn getFoldLaunchFn(int dtype, int devOp) {
   LaunchFn* tabs[10] = {gLaunch_i8_fold, gLaunch_u8_fold, gLaunch_i32_fold, gLaunch_u32_fold, gLaunch_i64_fold,
                         gLaunch_u64_fold, gLaunch_f16_fold, gLaunch_f32_fold, gLaunch_f64_fold, gLaunch_bf16_fold};
+  if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
+  return tabs[dtype][devOp];
+}
+
+// the pair kernel (mscclPairKernel): LL, devOp Sum..Min
+LaunchFn getPairLaunchFn(int dtype, int devOp) {
+  LaunchFn* tabs[10] = {gLaunch_i8_pair, gLaunch_u8_pair, gLaunch_i32_pair, gLaunch_u32_pair, gLaunch_i64_pair,
+                        gLaunch_u64_pair, gLaunch_f16_pair, gLaunch_f32_pair, gLaunch_f64_pair, gLaunch_bf16_pair};
   if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
   return tabs[dtype][devOp];
 }

@@ -423,8 +423,9 @@ struct Interp {
     sendStep++;
   }
 
-  template <bool REPOLL>
-  __device__ void llFusedOp(const T* src, T* dst, const Shape s) {
+  // PRE (the pair kernel, runPair): pre[u] already holds this lane's source pack u of step 0
+  template <bool REPOLL, bool PRE = false>
+  __device__ void llFusedOp(const T* src, T* dst, const Shape s, const u32x4* pre = nullptr) {
     const int slotLines = uni(sc->llSlotLines);
     const int slotPacks = slotLines / 2;
     if (slotPacks > kNT * U) {  // several passes per step (NCCL_LL_BUFFSIZE raised): lockstep form
@@ -443,7 +444,8 @@ struct Interp {
     waitSendCredit<kLLFifoSlots>();
     llStepPacks(s, slotPacks, nlinesFull, 0, B, act, two);
 #pragma unroll
-    for (int u = 0; u < U; u++) v[u] = act[u] ? loadPack(srs, vec, B[u], s.n) : (u32x4){0, 0, 0, 0};
+    for (int u = 0; u < U; u++)
+      v[u] = !act[u] ? (u32x4){0, 0, 0, 0} : PRE ? pre[u] : loadPack(srs, vec, B[u], s.n);
     llSendLines(s, slotLines, nlinesFull, 0, min(s.npk, slotPacks), act, two, v);
     LAT_EV(12);
     for (int k = 0; k < nsteps; k++) {
@@ -1847,6 +1849,87 @@ struct Interp {
   }
 };
 
+// ---------------------------------------------------------------- the pair kernel
+template <typename T, int OP>
+struct PairRunner : Interp<T, OP, pLL> {
+  using I = Interp<T, OP, pLL>;
+  using I::PE;
+  using I::U;
+  // A pair-form schedule (transport.cc: algoUpload) in one pass (enqueue.cc: launchGroup): thread
+  // block b's program is one fused s + rrc of input chunk pairSrc + b * pairStride into chunk
+  // pairDst + b * pairStride, no dependency.  Everything runSmall would read from the image comes
+  // from the kernel arguments, so one memory round trip brings the connection records, the launch
+  // epoch and this lane's source packs of the first FIFO step (llFusedOp's cut), and the exchange
+  // starts right after it.  The values, FIFO steps and flags are runSmall's (a peer may run either).
+  __device__ __forceinline__ void run(const RankWork& w, int local) {
+    I& it = *this;
+    it.tid = threadIdx.x;
+    it.redArg = 0;
+    it.trace = nullptr;
+    it.nkBuf = nullptr;
+    const int split = w.split;
+    const int lg = __builtin_ctz((unsigned)split);
+    const int bid = local >> lg, sub = local & (split - 1);
+    const int sizePer = (int)w.sizePerChunk;
+    const int cslot = bid * w.connSplit + sub;
+    DevSendConn* const sendG = w.send;
+    DevRecvConn* const recvG = w.recv;
+    uint64_t* const epochs = w.epochs;
+    const int maxSplit = w.maxSplit;
+    const int stride = w.pairStride;
+    T* const src = (T*)w.sendbuff + (int64_t)(w.pairSrc + bid * stride) * sizePer;
+    T* const dst = (T*)(w.pairDstBuf ? w.recvbuff : w.sendbuff) + (int64_t)(w.pairDst + bid * stride) * sizePer;
+    pinArgs(split, sizePer, cslot, sendG, recvG, epochs, maxSplit, src, dst);
+    // this workgroup's positions of the chunk (runSmall's cut for one chunk of nelem = sizePer)
+    const uint32_t Qc = ((uint32_t)sizePer + PE - 1) / PE;
+    Shape s;
+    s.n = sizePer;
+    s.Q = (int)Qc;
+    s.q0 = split == 1 ? 0 : (int)((Qc * (uint32_t)sub) >> lg);
+    s.Lq = split == 1 ? (int)Qc : (int)((Qc * (uint32_t)(sub + 1)) >> lg) - s.q0;
+    s.npk = s.Lq;
+    // one round trip: this lane's packs q = tid + u * kNT of step 0 (llFusedOp uses those with
+    // q < min(npk, slot packs) <= kNT * U), both connection records (wave 7), the epoch (wave 6)
+    u32x4 pre[U];
+    {
+      const __amdgpu_buffer_rsrc_t srs = makeRsrc(src);
+      const bool vec = I::aligned16(src);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const int q = it.tid + u * kNT;
+        pre[u] = q < s.npk ? it.loadPack(srs, vec, s.bufPack(q), s.n) : (u32x4){0, 0, 0, 0};
+      }
+      if (it.tid >= 448 && it.tid < 456) {
+        const int j = it.tid - 448;
+        const u32x4* from = j < 4 ? (const u32x4*)(sendG + cslot) + j : (const u32x4*)(recvG + cslot) + (j - 4);
+        u32x4* to = j < 4 ? (u32x4*)&it.sh->sconn + j : (u32x4*)&it.sh->rconn + (j - 4);
+        *to = *from;
+      }
+      if (it.tid == 384) {
+        it.sh->aborted = 0;
+        it.sh->epoch = atomicLoadAgent(epochs + bid * maxSplit + sub);
+      }
+    }
+    it.comm = w.comm;
+    it.timeoutTicks = w.timeoutTicks;
+    it.llFlagMask = w.llFlagMask;
+    it.llCleanMask = w.llCleanMask;
+    it.refNthreads = w.refNthreads;
+    __syncthreads();
+    const uint64_t workIndex = uni(it.sh->epoch);
+    it.scG = sendG + cslot;
+    it.rcG = recvG + cslot;
+    it.sc = &it.sh->sconn;
+    it.rc = &it.sh->rconn;
+    it.sendStep = uni(it.sh->sconn.step);
+    it.recvStep = uni(it.sh->rconn.step);
+    it.headSeen = uni(it.sh->sconn.headSeen);
+    it.tailSeen = uni(it.sh->rconn.tailSeen);
+    [[clang::always_inline]] it.template llFusedOp<true, true>(src, dst, s, pre);
+    it.epilogue(w, bid, sub, workIndex);
+  }
+};
+
 // The rank of the launch that owns block b: ranks' blocks are consecutive ([blockBase, blockBase +
 // nBlocks) in rank order), so r = the number of ranks i >= 1 whose blocks start at or below b.  All
 // R block bases are independent kernel-argument loads issued together (a search loop over them
@@ -1904,6 +1987,17 @@ __global__ void __launch_bounds__(kNT, 4) mscclSmallKernel(const LaunchArgsN<R> 
   Interp<T, OP, PROTO> it;
   it.sh = &sh;
   it.template runSmall<SET>(w, b - w.blockBase);
+}
+
+// The pair kernel (PairRunner): every RankWork of the launch is a pair-form schedule in one pass.
+template <typename T, int OP, int R>
+__global__ void __launch_bounds__(kNT, 4) mscclPairKernel(const LaunchArgsN<R> args) {
+  __shared__ BlockShared sh;
+  const int b = blockIdx.x;
+  const RankWork& w = rankWorkOf(args, b);
+  PairRunner<T, OP> it;
+  it.sh = &sh;
+  it.run(w, b - w.blockBase);
 }
 
 // The flat tree's fold kernel (Interp::runFold): rank r of the launch owns workgroups

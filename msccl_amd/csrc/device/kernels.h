@@ -69,6 +69,30 @@ int launchFoldKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// the pair kernel (mscclPairKernel, LL, Sum..Min): same contract as launchSmallKernel
+template <typename T, int OP>
+int launchPairKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  constexpr int RC = kCompactLaunchRanks;
+  if (gridBlocks == kQueryResidency) {
+    int n = 0, m = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclPairKernel<T, OP, kMaxLaunchRanks>, kNT, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, mscclPairKernel<T, OP, RC>, kNT, 0) != hipSuccess)
+      return 0;
+    return n < m ? n : m;
+  }
+  if (args.nRanks <= RC) {
+    LaunchArgsN<RC> a;
+    a.nRanks = args.nRanks;
+    a.pad = 0;
+    for (int r = 0; r < RC; r++) a.w[r] = args.w[r];
+    hipLaunchKernelGGL((mscclPairKernel<T, OP, RC>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL((mscclPairKernel<T, OP, kMaxLaunchRanks>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream,
+                       args);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // nRanks == 1 with a user PreMulSum op: dst = src * scale (the reference's oneRankReduce,
 // onerank_reduce.cu:12-44: ReduceOrCopyMulti with the preOp applied, postOp identity).
 template <typename T>
@@ -107,7 +131,9 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
       {launchSmallKernel<T, kSum, pLL, kSetExchange>, launchSmallKernel<T, kProd, pLL, kSetExchange>,       \
        launchSmallKernel<T, kMax, pLL, kSetExchange>, launchSmallKernel<T, kMin, pLL, kSetExchange>}};      \
   LaunchFn NAME##_fold[4] = {launchFoldKernel<T, kSum>, launchFoldKernel<T, kProd>, launchFoldKernel<T, kMax>, \
-                             launchFoldKernel<T, kMin>};
+                             launchFoldKernel<T, kMin>};                                                   \
+  LaunchFn NAME##_pair[4] = {launchPairKernel<T, kSum>, launchPairKernel<T, kProd>, launchPairKernel<T, kMax>, \
+                             launchPairKernel<T, kMin>};
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \
                          {launchKernel<T, kSumPostDiv, pLL>, nullptr, launchKernel<T, kSumPostDiv, pSimple>}}; \

@@ -267,6 +267,14 @@ RankWork makeWork(Planned& p) {
   w.merge = (uint8_t)merge;
   w.refNthreads = (int16_t)p.plan.refNthreads;
   w.maxAllowedCount = (uint8_t)p.plan.maxAllowedCount;
+  w.pairSrc = -1;
+  if ((size_t)p.plan.algoIndex < comm->algoPair.size() && p.plan.proto == kProtoLL) {
+    const ncclComm::PairForm& pf = comm->algoPair[p.plan.algoIndex];
+    w.pairSrc = (int16_t)pf.src;
+    w.pairDst = (int16_t)pf.dst;
+    w.pairStride = (int16_t)pf.stride;
+    w.pairDstBuf = (uint8_t)pf.dstBuf;
+  }
   w.launchSeq = comm->workIndex++;
   comm->last = {p.plan.algoIndex, p.plan.proto, split, merge, 0, 0, w.nBlocks};
   return w;
@@ -347,12 +355,21 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
     if (p->plan.ringColl != 0 || (size_t)p->plan.algoIndex >= c->algoSet.size() || c->algoSet[p->plan.algoIndex] != kSetExchange)
       set = kSetAll;
   }
+  // the pair kernel (interpreter.h: PairRunner) when every work is a pair-form schedule whose call
+  // is one pass of runSmall's loop, untraced
+  bool pair = small && !fold && set == kSetExchange && p0.op.comm->knobs.pairKernel;
+  for (int i = 0; i < args.nRanks && pair; i++) {
+    const RankWork& w = args.w[i];
+    pair = w.pairSrc >= 0 && w.trace == nullptr && w.sizePerChunk <= w.chunkSize * std::max<int>(1, w.merge);
+  }
   LaunchFn fn = fold ? getFoldLaunchFn(p0.plan.dtype, p0.op.devOp)
+                     : pair ? getPairLaunchFn(p0.plan.dtype, p0.op.devOp)
                      : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp, set)
                              : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
   for (Planned* p : ps) {
     p->op.comm->last.small = fold ? 2 : small ? 1 : 0;
     p->op.comm->last.set = small ? set : 0;
+    p->op.comm->last.pair = pair ? 1 : 0;
   }
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {

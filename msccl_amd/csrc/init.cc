@@ -142,6 +142,7 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   }
   s.knobs = comm->knobs;
   s.knobs.smallKernel = 0;  // a rank-local choice: both kernels cut the same FIFO steps
+  s.knobs.pairKernel = 0;   // likewise
   return s;
 }
 
@@ -177,6 +178,7 @@ static std::string knobDiff(const Knobs& a, const Knobs& b) {
 ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   Knobs agreed = comm->knobs;
   agreed.smallKernel = 0;
+  agreed.pairKernel = 0;
   for (size_t r = 0; r < recs.size(); r++) {
     if (memcmp(&recs[r].knobs, &agreed, sizeof(Knobs)) != 0) {
       WARN("MSCCL: rank %zu runs with different settings than rank %d: %s (they shape the FIFO steps and must "

@@ -80,6 +80,7 @@ Knobs Knobs::fromEnv() {
   k.treeOn = listEnables(getenv("NCCL_ALGO"), "Tree", true);
   k.treeMaxBytes = envInt("MSCCL_AMD_TREE_MAX_BYTES", -1);  // -1: the defaults of makeRingPlan / makeFlatTreePlan
   k.smallKernel = envInt("MSCCL_AMD_SMALL_KERNEL", 1) != 0;
+  k.pairKernel = envInt("MSCCL_AMD_PAIR_KERNEL", 1) != 0;
   k.fuse = envInt("MSCCL_AMD_FUSE", 1) != 0;
   k.treeFlat = envInt("MSCCL_AMD_TREE_FLAT", 1) != 0;
   k.lower = envInt("MSCCL_AMD_LOWER", 1) != 0;

@@ -81,6 +81,7 @@ struct Knobs {
   int32_t lower;             // MSCCL_AMD_LOWER: one-hop AllReduce schedules run as the fold (lower.cc)
   int32_t simpleBuffEnv;     // NCCL_BUFFSIZE was set (else a communicator of one GPU takes kLocalSimpleBuff)
   int64_t lowerMaxBytes;     // MSCCL_AMD_LOWER_MAX_BYTES: largest call (bytes per rank) lowered (-1: by ranks)
+  int32_t pairKernel;        // MSCCL_AMD_PAIR_KERNEL: pair-form exchanges take mscclPairKernel (rank-local)
   static Knobs fromEnv();
 };
 

@@ -637,6 +637,31 @@ ncclResult_t algoUpload(ncclComm* comm) {
       putImage(img, (size_t)b * stride, h, ts, tb.depBid, tb.depStep, tb.redSrcOff);
     }
     comm->algoSet[g] = exchangeOnly ? kSetExchange : kSetAll;
+    // the pair form (the pair kernel, interpreter.h: PairRunner): every thread block runs exactly
+    // one fused exchange (both ends agreed to fuse it) of one input chunk at an affine chunk index,
+    // its rrc reading that chunk and writing the same index of the input or output, no dependency
+    if (g >= comm->algoPair.size()) comm->algoPair.resize(g + 1);
+    ncclComm::PairForm pf;
+    bool pair = exchangeOnly && a.nBlocks > 0 && g < comm->algoFuse.size();
+    for (int b = 0; pair && b < a.nBlocks; b++) {
+      const std::vector<Transfer>& ts = a.tbs[b].transfers;
+      bool fused = false;
+      for (const FuseCandidate& f : comm->algoFuse[g]) fused |= f.tb == b && f.index == 0;
+      pair = fused && ts.size() == 2 && ts[0].type == kSend && ts[1].type == kRecvReduceCopy && ts[0].count == 1 &&
+             ts[1].count == 1 && ts[0].srcbuf == 0 && ts[1].srcbuf == 0 && ts[1].srcoff == ts[0].srcoff &&
+             ts[1].dstbuf <= 1 && ts[0].numDeps == 0 && ts[1].numDeps == 0 && ts[0].hasDep == 0 && ts[1].hasDep == 0;
+      if (!pair) break;
+      if (b == 0) {
+        pf.src = ts[0].srcoff;
+        pf.dst = ts[1].dstoff;
+        pf.dstBuf = ts[1].dstbuf;
+      } else if (b == 1) {
+        pf.stride = ts[0].srcoff - pf.src;
+      }
+      pair = ts[0].srcoff == pf.src + b * pf.stride && ts[1].dstoff == pf.dst + b * pf.stride &&
+             ts[1].dstbuf == pf.dstBuf;
+    }
+    comm->algoPair[g] = pair && pf.src < 32767 && pf.dst < 32767 ? pf : ncclComm::PairForm();
     NCCLCHECK(uploadImages(img, &d));
   }
   return ringUpload(comm);

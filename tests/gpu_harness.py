@@ -124,6 +124,7 @@ def run_collective(xml_text: str, nranks: int, coll: int, count: int, dt: int, o
             if err != 0:
                 raise M.NcclError(err, "kernel (async error)")
         gpu = [from_torch(t, N.storage(dt) if coll != L.ALLGATHER else N.storage(dt)) for t in t_out]
+        run_collective.last = [c.info()["last"] for c in comms]  # the kernel each rank's last launch took
     finally:
         for c in comms:
             c.destroy()

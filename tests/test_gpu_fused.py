@@ -185,3 +185,112 @@ def test_allgather_send_copy_fused(n, proto, count, dt, tmp_path, monkeypatch):
         _check(got, want, "AllGather fuse=%s" % fuse)
         res[fuse] = got
     _check(res["1"], res["0"], "AllGather fused vs unfused")
+
+
+# ---------------------------------------------------------------------------------------------
+# The pair kernel (interpreter.h: PairRunner): a pair-form schedule (every thread block one fused
+# s + rrc of affine chunks, transport.cc: pair form) whose call is one pass runs without the
+# image interpreter.  Same FIFO steps as the small kernel, so the values must be the oracle's and
+# bit-identical to MSCCL_AMD_PAIR_KERNEL=0's.
+@pytest.mark.parametrize("inst,count,dt,op,inplace", [
+    (1, 2048, 7, 0, True), (1, 3000, 7, 0, True), (16, 1 << 18, 7, 0, True), (16, 1 << 20, 9, 0, True),
+    (4, 1 << 16, 6, 2, True), (2, 10003 * 2, 6, 1, True), (4, 1 << 16, 2, 3, True), (1, 12345, 0, 0, True),
+    (16, 1 << 19, 8, 0, True), (4, 1 << 14, 7, 0, False), (16, 77776, 9, 2, False),
+])
+def test_pair_kernel_matches_oracle_and_small_kernel(inst, count, dt, op, inplace, tmp_path, monkeypatch):
+    xml = xmlgen.allreduce_pair_oneshot(inst, "LL", inplace=inplace)
+    monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "0")
+    res = {}
+    for pk in ("1", "0"):
+        monkeypatch.setenv("MSCCL_AMD_PAIR_KERNEL", pk)
+        got, want, _ = run_collective(xml, 2, L.ALLREDUCE, count, dt, op, inplace, seed=31, tmpdir=str(tmp_path))
+        last = run_collective.last
+        assert all(l["small"] == 1 and l["pair"] == (pk == "1") for l in last), last
+        _check(got, want, "pair kernel=%s" % pk)
+        res[pk] = got
+    _check(res["1"], res["0"], "pair vs small kernel")
+
+
+def test_pair_kernel_across_ll_cleanup(tmp_path, monkeypatch):
+    """24 pair-kernel launches across the 8-bit flag wrap and its cleanup steps (as
+    test_fused_across_ll_cleanup); Max keeps the in-place result the oracle's."""
+    monkeypatch.setenv("MSCCL_AMD_TEST_LL_CLEANUP", "1")
+    monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "0")
+    xml = xmlgen.allreduce_pair_oneshot(16, "LL")
+    got, want, _ = run_collective(xml, 2, L.ALLREDUCE, 1 << 18, 7, 2, True, seed=6, iters=24,
+                                  tmpdir=str(tmp_path))
+    assert all(l["pair"] == 1 for l in run_collective.last), run_collective.last
+    _check(got, want, "pair kernel cleanup")
+
+
+def test_pair_kernel_leaves_multi_pass_calls_to_other_kernels(tmp_path, monkeypatch):
+    """A call of more than one pass (1 instance, 4 MiB) keeps the general kernel."""
+    monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "0")
+    xml = xmlgen.allreduce_pair_oneshot(1, "LL")
+    got, want, _ = run_collective(xml, 2, L.ALLREDUCE, 1 << 20, 7, 0, True, seed=3, tmpdir=str(tmp_path))
+    assert all(l["pair"] == 0 for l in run_collective.last), run_collective.last
+    _check(got, want, "multi-pass")
+
+
+def _pair_mixed_proc(rank, world, xml_path, count, env, q_in, q_out):
+    import torch
+    os.environ["MSCCL_XML_FILES"] = xml_path
+    os.environ["MSCCL_AMD_TIMEOUT_SEC"] = "30"
+    os.environ["MSCCL_AMD_LOWER_MAX_BYTES"] = "0"
+    os.environ.update(env)
+    torch.cuda.set_device(0)
+    uid = M.get_unique_id() if rank == 0 else None
+    if rank == 0:
+        for _ in range(world - 1):
+            q_in.put(uid)
+    else:
+        uid = q_in.get(timeout=60)
+    x = gen_inputs(world, count, 7, 9)[rank]
+    comm = M.Comm.init_rank(world, uid, rank)
+    t = to_torch(x, torch.device("cuda:0"))
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        comm.all_reduce(t.data_ptr(), t.data_ptr(), count, M.FLOAT32, M.SUM, s)
+    torch.cuda.synchronize()
+    info = comm.info()
+    out = t.cpu().numpy()
+    err = comm.async_error()
+    comm.destroy()
+    q_out.put((rank, err, info["last"]["small"], info["last"].get("pair", 0), out))
+
+
+@pytest.mark.parametrize("peer", ["general", "small"])
+def test_pair_kernel_interoperates_with_other_kernels(peer, tmp_path):
+    """Rank 0 runs the pair kernel, rank 1 the general kernel (s, then rrc) or the small kernel's
+    fused exchange: one pass of 16 workgroups, three calls, the oracle's values."""
+    import torch.multiprocessing as mp
+    from oracle import plan as P, sim as S
+    world, count = 2, 1 << 18
+    xml = xmlgen.allreduce_pair_oneshot(16, "LL")
+    p = tmp_path / "pair16.xml"
+    p.write_text(xml)
+    env1 = {"MSCCL_AMD_SMALL_KERNEL": "0"} if peer == "general" else {"MSCCL_AMD_PAIR_KERNEL": "0"}
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_pair_mixed_proc, args=(r, world, str(p), count, {} if r == 0 else env1, q_in, q_out))
+          for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, small, pair, out = q_out.get(timeout=300)
+        res[r] = (err, small, pair, out)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert res[0][2] == 1 and res[1][2] == 0, (res[0], res[1])
+    assert res[1][1] == (0 if peer == "general" else 1)
+    algos = [L.parse_xml(xml, r, world) for r in range(world)]
+    call = P.Call(L.ALLREDUCE, count, 7, 0, world, 0, True)
+    plan = P.make_plan([algos[0]], call, 0)
+    ins = gen_inputs(world, count, 7, 9)
+    for _ in range(3):
+        ins, _st = S.run(algos, plan, ins, [None] * world, L.ALLREDUCE, True)
+    for r in range(world):
+        assert res[r][0] == 0
+        assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))

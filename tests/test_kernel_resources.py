@@ -61,6 +61,11 @@ def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
     assert len(small) == 3 * 4 * 2 * 2, sorted(small)
     for k, v in small.items():
         assert v.get("scratch", 1) == 0, (k, v)
+    # the pair kernel (interpreter.h: PairRunner), both argument blocks
+    pair = {k: v for k, v in ks.items() if re.search(r"mscclPairKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi(2|16)EE", k)}
+    assert len(pair) == 3 * 4 * 2, sorted(pair)
+    for k, v in pair.items():
+        assert v.get("scratch", 1) == 0, (k, v)
 
 
 # ---------------------------------------------------------------------------------------------

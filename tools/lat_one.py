@@ -113,9 +113,9 @@ def main():
     e1.record(stream)
     torch.cuda.synchronize()
     last = comms[0].info()["last"]
-    print("%s%s %d B x%d ranks: %.2f us per launch (events%s), host %.2f us per call; ran ringColl %d small %d" % (
+    print("%s%s %d B x%d ranks: %.2f us per launch (events%s), host %.2f us per call; ran ringColl %d small %d pair %d" % (
         a.schedule, "" if a.coll == "ar" else "-" + a.coll, a.bytes, a.ranks, e0.elapsed_time(e1) * 1000 / a.iters, ", graph replay" if graph else "",
-        host * 1e6, last["ringColl"], last["small"]), flush=True)
+        host * 1e6, last["ringColl"], last["small"], last.get("pair", 0)), flush=True)
     for c in comms:
         c.destroy()
 
