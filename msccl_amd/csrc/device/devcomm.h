@@ -227,6 +227,13 @@ struct RankWork {
   NpkitLog* npkit;              // MSCCL_AMD_NPKIT (null = off)
 };
 
+// Layout stamp of RankWork: every kernel object records the one it was compiled with (kernels.h)
+// and communicator setup refuses a library whose objects disagree with the host's
+// (dispatch.cc: kernelLayoutMismatch) -- a kernel object left over from before a RankWork change
+// reads its arguments at the wrong offsets, an illegal memory access rather than an error code.
+constexpr uint32_t kWorkLayout = (uint32_t)sizeof(RankWork) << 20 ^ (uint32_t)offsetof(RankWork, maxOpElems) << 10 ^
+                                 (uint32_t)offsetof(RankWork, npkit);
+
 template <int R>
 struct LaunchArgsN {
   int32_t nRanks;
@@ -263,6 +270,8 @@ LaunchFn getFoldLaunchFn(int dtype, int redop);   // mscclFoldKernel (the flat t
 // thread block: one fused s + rrc of one chunk at an affine chunk index, no dependency) in one
 // pass: no program image, the first FIFO step's source loaded with the connection records.
 LaunchFn getPairLaunchFn(int dtype, int redop);
+// the name of the first type whose kernel object was built with another RankWork layout, or null
+const char* kernelLayoutMismatch();
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):
 // NPKit's host/GPU clock calibration.  Returns 0 on a successful launch.
 int launchClockProbe(uint64_t* hostWord, void* stream);

@@ -3,7 +3,7 @@
 
 namespace msccl {
 #define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[2][4]; extern LaunchFn N##_fold[4]; \
-  extern LaunchFn N##_pair[4]; extern OneRankFn N##_one;
+  extern LaunchFn N##_pair[4]; extern OneRankFn N##_one; extern const uint32_t N##_layout;
 MSCCL_DECL(gLaunch_i8)
 MSCCL_DECL(gLaunch_u8)
 MSCCL_DECL(gLaunch_i32)
@@ -47,6 +47,17 @@ LaunchFn getPairLaunchFn(int dtype, int devOp) {
                         gLaunch_u64_pair, gLaunch_f16_pair, gLaunch_f32_pair, gLaunch_f64_pair, gLaunch_bf16_pair};
   if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
   return tabs[dtype][devOp];
+}
+
+const char* kernelLayoutMismatch() {
+  const uint32_t stamps[10] = {gLaunch_i8_layout, gLaunch_u8_layout, gLaunch_i32_layout, gLaunch_u32_layout,
+                               gLaunch_i64_layout, gLaunch_u64_layout, gLaunch_f16_layout, gLaunch_f32_layout,
+                               gLaunch_f64_layout, gLaunch_bf16_layout};
+  const char* names[10] = {"int8", "uint8", "int32", "uint32", "int64", "uint64", "float16", "float32", "float64",
+                           "bfloat16"};
+  for (int i = 0; i < 10; i++)
+    if (stamps[i] != kWorkLayout) return names[i];
+  return nullptr;
 }
 
 OneRankFn getOneRankFn(int dtype) {

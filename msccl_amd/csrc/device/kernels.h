@@ -133,7 +133,8 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
   LaunchFn NAME##_fold[4] = {launchFoldKernel<T, kSum>, launchFoldKernel<T, kProd>, launchFoldKernel<T, kMax>, \
                              launchFoldKernel<T, kMin>};                                                   \
   LaunchFn NAME##_pair[4] = {launchPairKernel<T, kSum>, launchPairKernel<T, kProd>, launchPairKernel<T, kMax>, \
-                             launchPairKernel<T, kMin>};
+                             launchPairKernel<T, kMin>};                                                   \
+  extern const uint32_t NAME##_layout = kWorkLayout;
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \
                          {launchKernel<T, kSumPostDiv, pLL>, nullptr, launchKernel<T, kSumPostDiv, pSimple>}}; \

@@ -66,6 +66,11 @@ void analyzeLowering(ncclComm* comm) {
 // Per-rank device state that does not depend on peers.
 ncclResult_t commLocalSetup(ncclComm* comm) {
   NCCLCHECK(hipErr(hipSetDevice(comm->cudaDev), "hipSetDevice"));
+  if (const char* stale = kernelLayoutMismatch()) {
+    WARN("MSCCL: the %s kernels were built with another RankWork layout than the host code (a stale kernel "
+         "object: rebuild the library)", stale);
+    return ncclInternalError;
+  }
   if (comm->nRanks > 1) NCCLCHECK(loadAlgos(comm));
   // 0 (default) = waits never time out, as in the reference; > 0 bounds every single wait
   comm->timeoutSec = (double)std::max<int64_t>(0, envInt("MSCCL_AMD_TIMEOUT_SEC", 0));

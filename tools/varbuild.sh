@@ -11,5 +11,5 @@ mkdir -p $B tools/lat
   -Imsccl_amd/csrc -Iinclude --offload-arch=gfx950 -munsafe-fp-atomics -Wshadow -ffp-contract=off \
   -DMSCCL_SMALL_ONLY "$@" -Rpass-analysis=kernel-resource-usage -c msccl_amd/csrc/device/kernels_f32.hip -o $B/kernels_f32.o 2> $B/res.txt || { cat $B/res.txt; exit 1; }
 OBJS=$(ls build/obj/*.o build/obj/device/*.o | grep -v kernels_f32.o)
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT $OBJS $B/kernels_f32.o -lpthread
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--no-undefined -o $OUT $OBJS $B/kernels_f32.o -lpthread
 echo built $OUT

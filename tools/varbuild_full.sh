@@ -16,5 +16,5 @@ done
 for p in "${pids[@]}"; do wait $p; done
 OBJS=$(ls build/obj/*.o build/obj/device/*.o)
 for t in $TYPES; do OBJS=$(echo "$OBJS" | grep -v "kernels_$t.o"); done
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $OUT $OBJS $B/kernels_*.o -lpthread
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--no-undefined -o $OUT $OBJS $B/kernels_*.o -lpthread
 echo built $OUT
