@@ -189,6 +189,10 @@ ncclResult_t transportConnect(ncclComm* comm, const std::vector<std::vector<Peer
 ncclResult_t algoUpload(ncclComm* comm);
 int algoSendRunOf(const Algorithm& a);
 std::vector<FuseCandidate> fusableTbs(const Algorithm& a);
+// The pair form of a schedule whose exchanges run fused as `fused` lists them (transport.cc), or
+// src -1.  A schedule in pair form on every rank with the pair kernel on everywhere is not lowered
+// by default (init.cc: applySplits): the pair kernel's fixed cost is the fold's or less.
+ncclComm::PairForm pairFormOf(const Algorithm& a, const std::vector<FuseCandidate>& fused);
 bool sendCopyFusable(const Algorithm& a, const std::vector<Transfer>& ts, size_t i);
 ncclResult_t ringUpload(ncclComm* comm);
 bool flatEnabled(const ncclComm* comm);  // the flat tree's connections and program exist

@@ -154,6 +154,14 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
         g.ngpus == nranks) {
       const FoldLowering fl = lowerScheduleFile(g.path, nranks);
       if (fl.ok) classes[a] = (int)fl.order.size();
+      // init.cc: applySplits keeps a schedule every rank runs with the pair kernel off the fold
+      bool pairEverywhere = k.lowerMaxBytes < 0 && k.fuse && k.pairKernel;
+      for (int r = 0; r < nranks && pairEverywhere; r++) {
+        Algorithm ar;
+        pairEverywhere = loadAlgoFromXml(g.path.c_str(), &ar, kMaxChannels, r, nranks) == 0 &&
+                         pairFormOf(ar, fusableTbs(ar)).src >= 0;
+      }
+      if (pairEverywhere) classes[a] = 0;
     }
   }
   if (useLocalSimpleFifo(oneGpu != 0, k, algos, sendRun)) k.buffSizes[kProtoSimple] = kLocalSimpleBuff;

@@ -124,6 +124,7 @@ struct SplitRecord {
   int32_t nFuse[kMaxAlgos];
   int16_t fuse[kMaxAlgos][kMaxFuse][2];  // (channel, peer) of each fusable exchange (fusableTbs)
   uint8_t lowered[kMaxAlgos];             // analyzeLowering found the schedule a one-hop fold
+  uint8_t pairRun[kMaxAlgos];             // in pair form when its offered exchanges fuse, pair kernel on
   Knobs knobs;
 };
 
@@ -139,6 +140,7 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
     s.lowered[a] = a < comm->algoFold.size() && !comm->algoFold[a].order.empty();
     const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
+    s.pairRun[a] = comm->knobs.fuse && comm->knobs.pairKernel && pairFormOf(comm->algos[a], fc).src >= 0;
     for (size_t i = 0; i < fc.size() && s.nFuse[a] < kMaxFuse; i++) {
       s.fuse[a][s.nFuse[a]][0] = fc[i].chan;
       s.fuse[a][s.nFuse[a]][1] = fc[i].peer;
@@ -227,10 +229,17 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   if (useLocalSimpleFifo(maxCo == (int)recs.size(), comm->knobs, comm->algos, comm->algoSendRun))
     comm->knobs.buffSizes[kProtoSimple] = kLocalSimpleBuff;
   // a schedule runs as the fold only when every rank found it one (the two ends of every flat
-  // connection must run the same kernel)
-  for (size_t a = 0; a < comm->algoFold.size() && a < (size_t)kMaxAlgos; a++)
-    for (auto& r : recs)
+  // connection must run the same kernel), and by default not when every rank runs it with the
+  // pair kernel: 2 ranks, 128 B - 4 KiB, one instance, graph replay: pair kernel 5.1-5.7 us
+  // against the fold's 5.4-6.2 (profiles/r05t_pair_small.txt)
+  for (size_t a = 0; a < comm->algoFold.size() && a < (size_t)kMaxAlgos; a++) {
+    bool pairEverywhere = comm->knobs.lowerMaxBytes < 0;
+    for (auto& r : recs) {
       if ((int)a >= r.nAlgos || !r.lowered[a]) comm->algoFold[a] = ncclComm::FoldProgram();
+      pairEverywhere = pairEverywhere && (int)a < r.nAlgos && r.pairRun[a];
+    }
+    if (pairEverywhere) comm->algoFold[a] = ncclComm::FoldProgram();
+  }
   // an exchange runs fused only when both ends offered it (fusableTbs)
   comm->algoFuse.assign(comm->algos.size(), {});
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos && comm->knobs.fuse; a++) {

@@ -597,6 +597,32 @@ bool sendCopyFusable(const Algorithm& a, const std::vector<Transfer>& ts, size_t
   return (s0 == d0) || s1 <= d0 || d1 <= s0;
 }
 
+// The pair form (the pair kernel, interpreter.h: PairRunner): every thread block runs exactly one
+// fused exchange (listed in `fused`) of one input chunk at an affine chunk index, its rrc reading
+// that chunk and writing the same index of the input or output, no dependency.
+ncclComm::PairForm pairFormOf(const Algorithm& a, const std::vector<FuseCandidate>& fused) {
+  ncclComm::PairForm pf;
+  bool pair = a.nBlocks > 0;
+  for (int b = 0; pair && b < a.nBlocks; b++) {
+    const std::vector<Transfer>& ts = a.tbs[b].transfers;
+    bool f = false;
+    for (const FuseCandidate& c : fused) f |= c.tb == b && c.index == 0;
+    pair = f && ts.size() == 2 && ts[0].type == kSend && ts[1].type == kRecvReduceCopy && ts[0].count == 1 &&
+           ts[1].count == 1 && ts[0].srcbuf == 0 && ts[1].srcbuf == 0 && ts[1].srcoff == ts[0].srcoff &&
+           ts[1].dstbuf <= 1 && ts[0].numDeps == 0 && ts[1].numDeps == 0 && ts[0].hasDep == 0 && ts[1].hasDep == 0;
+    if (!pair) break;
+    if (b == 0) {
+      pf.src = ts[0].srcoff;
+      pf.dst = ts[1].dstoff;
+      pf.dstBuf = ts[1].dstbuf;
+    } else if (b == 1) {
+      pf.stride = ts[0].srcoff - pf.src;
+    }
+    pair = ts[0].srcoff == pf.src + b * pf.stride && ts[1].dstoff == pf.dst + b * pf.stride && ts[1].dstbuf == pf.dstBuf;
+  }
+  return pair && pf.src < 32767 && pf.dst < 32767 ? pf : ncclComm::PairForm();
+}
+
 // Pack every algorithm's per-tb programs into fixed-stride images and upload them (replaces
 // the 29 MB mscclDevCommInfo copy of devCommSetup, init.cc:300-304).
 ncclResult_t algoUpload(ncclComm* comm) {
@@ -637,31 +663,8 @@ ncclResult_t algoUpload(ncclComm* comm) {
       putImage(img, (size_t)b * stride, h, ts, tb.depBid, tb.depStep, tb.redSrcOff);
     }
     comm->algoSet[g] = exchangeOnly ? kSetExchange : kSetAll;
-    // the pair form (the pair kernel, interpreter.h: PairRunner): every thread block runs exactly
-    // one fused exchange (both ends agreed to fuse it) of one input chunk at an affine chunk index,
-    // its rrc reading that chunk and writing the same index of the input or output, no dependency
     if (g >= comm->algoPair.size()) comm->algoPair.resize(g + 1);
-    ncclComm::PairForm pf;
-    bool pair = exchangeOnly && a.nBlocks > 0 && g < comm->algoFuse.size();
-    for (int b = 0; pair && b < a.nBlocks; b++) {
-      const std::vector<Transfer>& ts = a.tbs[b].transfers;
-      bool fused = false;
-      for (const FuseCandidate& f : comm->algoFuse[g]) fused |= f.tb == b && f.index == 0;
-      pair = fused && ts.size() == 2 && ts[0].type == kSend && ts[1].type == kRecvReduceCopy && ts[0].count == 1 &&
-             ts[1].count == 1 && ts[0].srcbuf == 0 && ts[1].srcbuf == 0 && ts[1].srcoff == ts[0].srcoff &&
-             ts[1].dstbuf <= 1 && ts[0].numDeps == 0 && ts[1].numDeps == 0 && ts[0].hasDep == 0 && ts[1].hasDep == 0;
-      if (!pair) break;
-      if (b == 0) {
-        pf.src = ts[0].srcoff;
-        pf.dst = ts[1].dstoff;
-        pf.dstBuf = ts[1].dstbuf;
-      } else if (b == 1) {
-        pf.stride = ts[0].srcoff - pf.src;
-      }
-      pair = ts[0].srcoff == pf.src + b * pf.stride && ts[1].dstoff == pf.dst + b * pf.stride &&
-             ts[1].dstbuf == pf.dstBuf;
-    }
-    comm->algoPair[g] = pair && pf.src < 32767 && pf.dst < 32767 ? pf : ncclComm::PairForm();
+    comm->algoPair[g] = exchangeOnly && g < comm->algoFuse.size() ? pairFormOf(a, comm->algoFuse[g]) : ncclComm::PairForm();
     NCCLCHECK(uploadImages(img, &d));
   }
   return ringUpload(comm);

@@ -294,3 +294,19 @@ def test_pair_kernel_interoperates_with_other_kernels(peer, tmp_path):
     for r in range(world):
         assert res[r][0] == 0
         assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
+
+
+@pytest.mark.parametrize("nbytes", [128, 4092, 8192, 1 << 20])
+def test_c2_tiers_take_the_pair_kernel(nbytes, tmp_path, monkeypatch):
+    """bench.py's C2 tiers with default settings: every one-pass size runs the pair kernel (small
+    calls included: the pair form is not lowered by default), the oracle's values."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.delenv("MSCCL_AMD_LOWER_MAX_BYTES", raising=False)
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    path = [t[3] for t in tiers if t[0] <= nbytes < t[1]][0]
+    got, want, _ = run_collective(open(path).read(), 2, L.ALLREDUCE, nbytes // 4, 7, 0, True, seed=nbytes % 91,
+                                  tmpdir=str(tmp_path))
+    assert all(l["pair"] == 1 and l["ringColl"] == 0 for l in run_collective.last), run_collective.last
+    _check(got, want, "C2 tier %d B" % nbytes)

@@ -70,9 +70,11 @@ def test_c3_oneshot_tier_lowered(tmp_path, nbytes, dt):
 
 
 @pytest.mark.parametrize("op", [0, 1, 2, 3])
-def test_unordered_oneshot_every_op(tmp_path, op):
+def test_unordered_oneshot_every_op(tmp_path, op, monkeypatch):
     """The unordered one-shot: every rank folds its own input first (a different order per rank,
-    different fp16 bits per rank), out of place too."""
+    different fp16 bits per rank), out of place too (the pair exchange lowered by an explicit
+    limit: by default it runs the pair kernel, init.cc: applySplits)."""
+    monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "4096")
     xml = xmlgen.allreduce_oneshot(4, 2, "LL")
     with CoResident(4, [xml], str(tmp_path)) as cr:
         last, _ = _case(cr, 2 * 1000, 6, 20 + op, op=op)

@@ -107,3 +107,22 @@ def test_fallback_and_ll128_remote(tmp_path):
     assert got["kernel"] == "fold" and got["algo"] == -1, got
     got = M.launch_plan_json(files, 0, 4, False, L.ALLREDUCE, (8 << 20) + 1, 7, 0, True)
     assert got["kernel"] == "ring", got
+
+
+def test_pair_form_schedule_keeps_the_pair_kernel(tmp_path, monkeypatch):
+    """A schedule in pair form (every thread block one fused s + rrc, transport.cc: pairFormOf) is
+    not lowered by default on either placement: the pair kernel's fixed cost is the fold's or less
+    (init.cc: applySplits).  An explicit MSCCL_AMD_LOWER_MAX_BYTES, MSCCL_AMD_PAIR_KERNEL=0 or
+    MSCCL_AMD_FUSE=0 brings the fold back; the two-phase all-pairs (not pair form) stays lowered."""
+    files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(1, "LL")])
+    for one_gpu in (True, False):
+        got = M.launch_plan_json(files, 0, 2, one_gpu, L.ALLREDUCE, 32, 7, 0, True)
+        assert got["kernel"] == "interpreter" and got["classes"] == [0], got
+    for env in (("MSCCL_AMD_LOWER_MAX_BYTES", "4096"), ("MSCCL_AMD_PAIR_KERNEL", "0"), ("MSCCL_AMD_FUSE", "0")):
+        monkeypatch.setenv(*env)
+        got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 32, 7, 0, True)
+        assert got["kernel"] == "fold" and got["classes"] == [1], (env, got)
+        monkeypatch.delenv(env[0])
+    files = _files(tmp_path, [xmlgen.allreduce_allpairs(2, 4, "LL")])
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 32, 7, 0, True)
+    assert got["kernel"] == "fold", got
