@@ -299,7 +299,8 @@ def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out, one_gpu=False, env=Non
             comm.all_gather(x.data_ptr(), t.data_ptr(), count, dt, s)
         torch.cuda.synchronize()
         outs.append(t.cpu().numpy())
-        kernels.append(comm.info()["last"]["small"])  # 0 general, 1 small, 2 fold kernel
+        last = comm.info()["last"]
+        kernels.append(3 if last.get("pair") else last["small"])  # 0 general, 1 small, 2 fold, 3 pair kernel
     err = comm.async_error()
     remote = comm.info()["anyRemote"]
     comm.destroy()
@@ -469,3 +470,44 @@ def test_four_processes_one_gpu_bench_tiers(tmp_path):
     res = _eight_processes(tmp_path, xmls, jobs, world=4, one_gpu=True)
     _check_four(res, xmls, jobs)
     assert [res[0][2][j] for j in range(3)] == [2, 2, 1]
+
+
+# ------------------------------------------------------------------------------------------------
+# two ranks: bench.py --gpus 2 (C2: fp32, one rank per GPU, the pair exchange tiers)
+
+def _two_rank_job(tmp_path, remote):
+    b = _bench()
+    tiers = b.make_xmls(2, "LL", 16, str(tmp_path), remote=remote)
+    xmls = [open(t[3]).read() for t in tiers]
+    sizes = (128, 4096, 8192, 1 << 20, 32 << 20)
+    return xmls, [(L.ALLREDUCE, nb // 4, 7, 80 + k) for k, nb in enumerate(sizes)]
+
+
+def _check_two(res, xmls, jobs):
+    for j, (coll, count, dt, seed) in enumerate(jobs):
+        want = _oracle(xmls, coll, count, dt, seed, True, world=2)
+        for r in range(2):
+            assert res[r][0] == 0
+            _check([res[r][1][j]], [want[r]], "2 processes job %d rank %d" % (j, r))
+
+
+@needs2
+def test_two_processes_two_devices_c2_tiers(tmp_path):
+    """bench.py --gpus 2: 2 rank processes on 2 GPUs (hipIpc over xGMI), C2's tiers 128 B - 32 MiB:
+    the pair kernel for every one-pass call, the small kernel's merged passes at 32 MiB, bit-exact
+    against the oracle."""
+    xmls, jobs = _two_rank_job(tmp_path, True)
+    res = _eight_processes(tmp_path, xmls, jobs, world=2)
+    _check_two(res, xmls, jobs)
+    assert all(res[r][3] == 1 for r in range(2))
+    assert res[0][2] == [3, 3, 3, 3, 1], res[0][2]
+
+
+def test_two_processes_one_gpu_forced_remote_c2_tiers(tmp_path):
+    """The same job with both processes on cuda:0 and every peer treated as remote
+    (MSCCL_AMD_FORCE_REMOTE=1: the cross-GPU limits and paths the N=2 driver run takes)."""
+    xmls, jobs = _two_rank_job(tmp_path, True)
+    res = _eight_processes(tmp_path, xmls, jobs, world=2, one_gpu=True, env={"MSCCL_AMD_FORCE_REMOTE": "1"})
+    _check_two(res, xmls, jobs)
+    assert all(res[r][3] == 1 for r in range(2))
+    assert res[0][2] == [3, 3, 3, 3, 1], res[0][2]
