@@ -132,3 +132,19 @@ def test_memory_asm_check_catches_an_sgpr_operand():
     reg = 'asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));'
     assert _bad_asm(ok) == [] and _bad_asm(reg) == []
     assert [c for _, c in _bad_asm(bad)] == ['"s"']
+
+
+def test_every_type_object_holds_every_kernel_family():
+    """Each per-type kernel object (build/obj/device/kernels_<type>.res) was compiled from the
+    current kernels.h: it lists the general, small, fold and pair kernels (a stale object once
+    lacked the pair kernel and read RankWork at old offsets; init.cc also checks the layout stamp
+    at run time)."""
+    files = sorted(glob.glob(os.path.join(RES, "kernels_*.res")))
+    files = [f for f in files if not re.search(r"kernels_(clock|probe)\.res$", f)]
+    if not files:
+        pytest.skip("no kernel resource reports (run __graft_entry__.build() first)")
+    assert len(files) == 10, files
+    for f in files:
+        text = open(f).read()
+        for fam in ("mscclKernel", "mscclSmallKernel", "mscclFoldKernel", "mscclPairKernel"):
+            assert re.search(r"Function Name: _ZN5msccl\d*%sI" % fam, text), (os.path.basename(f), fam)
