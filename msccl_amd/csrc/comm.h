@@ -91,6 +91,7 @@ struct ncclComm {
   bool ringFallback = true;        // MSCCL_AMD_RING_FALLBACK (default 1), same on every rank
   bool anyRemote = false;          // some peer runs on another GPU (xGMI): no LL128 unless allowed
   std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
+  std::vector<int> algoSplitBase;  // the split of the default budget (algoSplit is wider for 2 co-resident LL ranks)
   std::vector<int> algoSendRun;    // per algorithm: longest run of send chunks before a receive, max over
                                    // every rank's program (same on all ranks)
   std::vector<std::vector<msccl::FuseCandidate>> algoFuse;  // per algorithm: thread blocks running fused

@@ -235,6 +235,12 @@ RankWork makeWork(Planned& p) {
   // MSCCL_AMD_SPLIT is kept as is.
   if (comm->knobs.split <= 0)
     while (split > 1 && p.plan.sizePerChunk / pe < (int64_t)split * (kNT / 4)) split /= 2;
+  // the wide budget (two co-resident LL ranks, plan.h: kWideSplitMinBytes) only while every
+  // workgroup still moves kWideSplitMinBytes of the call; nBytes is the same on every rank
+  if ((size_t)p.plan.algoIndex < comm->algoSplitBase.size())
+    while (split > comm->algoSplitBase[p.plan.algoIndex] &&
+           p.plan.nBytes < (int64_t)da.nBlocks * split * kWideSplitMinBytes)
+      split /= 2;
   w.split = (uint8_t)split;
   w.nBlocks = (int16_t)(da.nBlocks * split);
   // Consecutive full interpreter iterations can run as one: every element still sees the same

@@ -208,6 +208,7 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   comm->coResident = 0;
   for (auto& q : recs) comm->coResident += !strcmp(mine.host, q.host) && !strcmp(mine.bus, q.bus);
   comm->algoSplit.assign(comm->algos.size(), 1);
+  comm->algoSplitBase.assign(comm->algos.size(), 1);
   comm->algoSendRun.assign(comm->algos.size(), 1);
   comm->maxSplit = 1;
   for (size_t a = 0; a < comm->algos.size(); a++) {
@@ -217,7 +218,10 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
         mb = std::max(mb, (int)r.nBlocks[a]);
         run = std::max(run, (int)r.sendRun[a]);
       }
-    comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs, comm->algos[a].proto);
+    // two ranks sharing a GPU: LL schedules get the wide budget for their large calls
+    const bool wide = maxCo == 2 && comm->algos[a].proto == kProtoLL;
+    comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs, comm->algos[a].proto, wide);
+    comm->algoSplitBase[a] = chooseSplit(mb, maxCo, comm->knobs, comm->algos[a].proto);
     comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
   }

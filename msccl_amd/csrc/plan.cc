@@ -96,7 +96,7 @@ bool useLocalSimpleFifo(bool oneGpu, const Knobs& k, const std::vector<Algorithm
   return true;
 }
 
-int chooseSplit(int maxBlocks, int coResident, const Knobs& kn, int proto) {
+int chooseSplit(int maxBlocks, int coResident, const Knobs& kn, int proto, bool wide) {
   int k = 1;
   if (kn.split > 0) {
     while (k * 2 <= kMaxSplit && k * 2 <= kn.split) k *= 2;
@@ -106,7 +106,7 @@ int chooseSplit(int maxBlocks, int coResident, const Knobs& kn, int proto) {
   // runs (profiles/r05g_target_wgs.txt): 8 co-resident ranks, LL fp16 all-pairs 2 MiB 48.0 ->
   // 41.8 us, 32 MiB 541 -> 532, RCCL's 8n-32tb file 602 -> 554 us (split 2 -> 1); the Simple C4
   // ring 1.49 ms at 512 against 1.76 at 256 (r05e_c4knobs.txt)
-  const int64_t target = kn.targetWgs > 0 ? kn.targetWgs : proto == kProtoSimple ? 512 : 256;
+  const int64_t target = kn.targetWgs > 0 ? kn.targetWgs : proto == kProtoSimple || wide ? 512 : 256;
   int64_t per = (int64_t)std::max(1, maxBlocks) * std::max(1, coResident);
   while (k * 2 <= kMaxSplit && per * k * 2 <= target) k *= 2;
   return k;

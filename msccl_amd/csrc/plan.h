@@ -111,8 +111,14 @@ int makePlan(const std::vector<Algorithm>& algos, int algoIndex, int protoOverri
 // has maxBlocks thread blocks when coResident ranks share a GPU: the largest power of two <=
 // kMaxSplit that keeps the GPU's workgroups within MSCCL_AMD_TARGET_WGS (default by protocol: 256
 // = one per CU for LL / LL128, 512 for Simple).  MSCCL_AMD_SPLIT forces a value.  Every rank must
-// compute the same value.
-int chooseSplit(int maxBlocks, int coResident, const Knobs& k, int proto);
+// compute the same value.  wide: the budget of two co-resident ranks' LL schedules, 512 (for large
+// calls; makeWork steps a call back towards the default split while a workgroup would move less
+// than kWideSplitMinBytes).
+int chooseSplit(int maxBlocks, int coResident, const Knobs& k, int proto, bool wide = false);
+// Two co-resident ranks, graph replay, same box (profiles/r05w_target_wgs.txt): the 2-rank two-phase
+// all-pairs x16 at 512 workgroups per GPU against 256: 4 MiB 25.5 against 23.1 us (16 KiB per
+// workgroup), 8 MiB 31.0 against 33.2, 16 MiB 46.5 against 52.5, 32 MiB 79.7 against 102.8.
+constexpr int64_t kWideSplitMinBytes = 32 << 10;
 // The reference's fallback when no MSCCL algorithm matches (enqueue.cc:461-476): a ring
 // AllReduce / ReduceScatter / AllGather (collectives/device/all_reduce.h:14-100,
 // reduce_scatter.h:13-67, all_gather.h:13-78).  Fills *p (algoIndex -1, ringColl set) and returns

@@ -155,3 +155,17 @@ def test_mixed_kernels_across_processes(tmp_path):
     for r in range(world):
         assert res[r][0] == 0
         assert np.array_equal(res[r][2].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
+
+
+@pytest.mark.parametrize("count,split", [(1 << 20, 4), (1 << 21, 8), (1 << 23, 8)])
+def test_two_rank_wide_split_by_call_size(tmp_path, count, split):
+    """Two co-resident ranks' LL schedules get the wide workgroup budget (plan.h: kWideSplitMinBytes):
+    the 2-rank two-phase all-pairs x16 (32 thread blocks) runs split 8 while every workgroup moves
+    32 KiB or more (8 and 32 MiB), split 4 below (4 MiB); the oracle's values either way."""
+    xml = xmlgen.allreduce_allpairs(2, 16, "LL")
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        ins, got, last = _run(cr, count, 7, 0, seed=count % 97)
+        assert all(l["split"] == split for l in last), last
+        want, _ = cr.oracle(L.ALLREDUCE, count, 7, 0, ins, True)
+        for r in range(2):
+            assert np.array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
