@@ -981,8 +981,39 @@ def measure_e2e(comms, n, nbytes, dt, ts, stream, dev):
     torch.cuda.synchronize()
     t = (time.perf_counter() - t0) / reps
     algbw = nbytes / t / 1e9
-    return {"bytes": nbytes, "ms": round(t * 1e3, 4), "algbw": round(algbw, 3),
-            "busbw": round(algbw * 2 * (n - 1) / n, 3)}
+    serial_out = [h.clone() for h in host_out]
+    from msccl_amd import hostpath
+    res = {"bytes": nbytes, "ms": round(t * 1e3, 4), "algbw": round(algbw, 3),
+           "busbw": round(algbw * 2 * (n - 1) / n, 3)}
+    # zero copy (msccl_amd/hostpath.py): the collective reads and writes the pinned buffers itself,
+    # in place on a pinned copy of the inputs (the tiers' XMLs are in place)
+    host_io = [h.clone().pin_memory() for h in host_in]
+    hostpath.all_reduce_host(comms, host_io, host_io, dt, M.SUM)
+    torch.cuda.synchronize()
+    same = all(torch.equal(a, b) for a, b in zip(host_io, serial_out))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        hostpath.all_reduce_host(comms, host_io, host_io, dt, M.SUM)
+    torch.cuda.synchronize()
+    tz = (time.perf_counter() - t0) / reps
+    res["zero_copy"] = {"ms": round(tz * 1e3, 4), "algbw": round(nbytes / tz / 1e9, 3),
+                        "same_bits_as_serial": bool(same)}
+    # staged: chunks through H2D / collective / D2H streams
+    chunk = hostpath.default_chunk_bytes(nbytes)
+    streams = {}
+    for o in host_out:
+        o.zero_()
+    hostpath.all_reduce_host_staged(comms, host_in, host_out, dbufs, dt, M.SUM, chunk, streams)
+    torch.cuda.synchronize()
+    same = all(torch.equal(a, b) for a, b in zip(host_out, serial_out))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        hostpath.all_reduce_host_staged(comms, host_in, host_out, dbufs, dt, M.SUM, chunk, streams)
+    torch.cuda.synchronize()
+    tp = (time.perf_counter() - t0) / reps
+    res["staged"] = {"ms": round(tp * 1e3, 4), "algbw": round(nbytes / tp / 1e9, 3), "chunk_bytes": chunk,
+                     "same_bits_as_serial": bool(same)}
+    return res
 
 
 if __name__ == "__main__":
