@@ -296,7 +296,7 @@ def test_pair_kernel_interoperates_with_other_kernels(peer, tmp_path):
         assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
 
 
-@pytest.mark.parametrize("nbytes", [128, 4092, 8192, 1 << 20])
+@pytest.mark.parametrize("nbytes", [128, 4092, 8192, 1 << 20, 32 << 20])
 def test_c2_tiers_take_the_pair_kernel(nbytes, tmp_path, monkeypatch):
     """bench.py's C2 tiers with default settings: every one-pass size runs the pair kernel (small
     calls included: the pair form is not lowered by default), the oracle's values."""
