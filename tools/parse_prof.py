@@ -36,7 +36,7 @@ def find(d, pattern):
 
 
 def is_msccl(name):
-    return "mscclKernel" in name or "mscclSmallKernel" in name or "mscclFoldKernel" in name
+    return any(k in name for k in ("mscclKernel", "mscclSmallKernel", "mscclFoldKernel", "mscclPairKernel"))
 
 
 def counter_avg(d, counter):
