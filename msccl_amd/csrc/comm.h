@@ -85,6 +85,7 @@ struct ncclComm {
     int src = -1, dst = 0, stride = 0, dstBuf = 0;
   };
   std::vector<PairForm> algoPair;
+  std::vector<uint8_t> algoPairAll;  // every rank runs the schedule in pair form (init.cc: applySplits)
   std::vector<msccl::DevAlgoHost> foldAlgos;
   msccl::DevAlgoHost ringAlgos[6];  // ring fallback programs, [4] = tree, [5] = flat tree (transport.cc: ringUpload)
   msccl::Knobs knobs;              // environment knobs, read once at init, identical on every rank

@@ -264,12 +264,13 @@ RankWork makeWork(Planned& p) {
     // as many full iterations per call as the bound allows: fewest dependency rounds
     // (C2 32 MiB LL: 348 GB/s with `split` iterations per call, 405 with all 16)
     const int64_t chunk = std::max<int64_t>(1, p.plan.chunkSize);
-    // A pair-form schedule (transport.cc: pairFormOf) has no run of sends: every thread block's
-    // only send is fused with its receive, one FIFO step ahead of it, on both ends.  So the bound
+    // A schedule in pair form on every rank (transport.cc: pairFormOf; init.cc: algoPairAll) has no
+    // run of sends: every thread block's only send is fused with its receive, one FIFO step ahead
+    // of it, on both ends.  So the bound
     // does not apply, and every full iteration merges into one pass (the pair kernel).  C2 32 MiB:
     // one pass instead of two.
-    const bool pairForm = p.plan.proto == kProtoLL && (size_t)p.plan.algoIndex < comm->algoPair.size() &&
-                          comm->algoPair[p.plan.algoIndex].src >= 0;
+    const bool pairForm = p.plan.proto == kProtoLL && (size_t)p.plan.algoIndex < comm->algoPairAll.size() &&
+                          comm->algoPairAll[p.plan.algoIndex];
     const int64_t fit = pairForm ? 64 : std::max<int64_t>(1, w.maxOpElems / (chunk * sendRun));
     merge = (int)std::min<int64_t>(envMerge > 0 ? envMerge : fit, fit);  // MSCCL_AMD_MERGE only lowers it
     // a merged iteration stays within 1 GiB, far inside a buffer descriptor's 2 GiB reach

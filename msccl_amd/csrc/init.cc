@@ -124,7 +124,8 @@ struct SplitRecord {
   int32_t nFuse[kMaxAlgos];
   int16_t fuse[kMaxAlgos][kMaxFuse][2];  // (channel, peer) of each fusable exchange (fusableTbs)
   uint8_t lowered[kMaxAlgos];             // analyzeLowering found the schedule a one-hop fold
-  uint8_t pairRun[kMaxAlgos];             // in pair form when its offered exchanges fuse, pair kernel on
+  uint8_t pairShape[kMaxAlgos];           // in pair form when its offered exchanges fuse (pairFormOf)
+  uint8_t pairRun[kMaxAlgos];             // pairShape and the pair kernel on
   Knobs knobs;
 };
 
@@ -140,7 +141,8 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
     s.lowered[a] = a < comm->algoFold.size() && !comm->algoFold[a].order.empty();
     const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
-    s.pairRun[a] = comm->knobs.fuse && comm->knobs.pairKernel && pairFormOf(comm->algos[a], fc).src >= 0;
+    s.pairShape[a] = comm->knobs.fuse && pairFormOf(comm->algos[a], fc).src >= 0;
+    s.pairRun[a] = s.pairShape[a] && comm->knobs.pairKernel;
     for (size_t i = 0; i < fc.size() && s.nFuse[a] < kMaxFuse; i++) {
       s.fuse[a][s.nFuse[a]][0] = fc[i].chan;
       s.fuse[a][s.nFuse[a]][1] = fc[i].peer;
@@ -243,6 +245,14 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
       pairEverywhere = pairEverywhere && (int)a < r.nAlgos && r.pairRun[a];
     }
     if (pairEverywhere) comm->algoFold[a] = ncclComm::FoldProgram();
+  }
+  // a schedule in pair form on every rank merges its calls into one pass (enqueue.cc: makeWork);
+  // the pass cut decides which workgroup owns which positions, so every rank must agree on it
+  comm->algoPairAll.assign(comm->algos.size(), 0);
+  for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) {
+    bool all = true;
+    for (auto& r : recs) all = all && (int)a < r.nAlgos && r.pairShape[a];
+    comm->algoPairAll[a] = all ? 1 : 0;
   }
   // an exchange runs fused only when both ends offered it (fusableTbs)
   comm->algoFuse.assign(comm->algos.size(), {});

@@ -259,13 +259,15 @@ def _pair_mixed_proc(rank, world, xml_path, count, env, q_in, q_out):
     q_out.put((rank, err, info["last"]["small"], info["last"].get("pair", 0), out))
 
 
+@pytest.mark.parametrize("count", [1 << 18, 1 << 23])
 @pytest.mark.parametrize("peer", ["general", "small"])
-def test_pair_kernel_interoperates_with_other_kernels(peer, tmp_path):
-    """Rank 0 runs the pair kernel, rank 1 the general kernel (s, then rrc) or the small kernel's
-    fused exchange: one pass of 16 workgroups, three calls, the oracle's values."""
+def test_pair_kernel_interoperates_with_other_kernels(peer, count, tmp_path):
+    """Rank 0 runs the pair kernel, rank 1 the general kernel or the small kernel's fused exchange:
+    one pass of 16 thread blocks (32 MiB: 64 iterations merged into it on both ranks, whatever
+    kernel each runs), three calls, the oracle's values."""
     import torch.multiprocessing as mp
     from oracle import plan as P, sim as S
-    world, count = 2, 1 << 18
+    world = 2
     xml = xmlgen.allreduce_pair_oneshot(16, "LL")
     p = tmp_path / "pair16.xml"
     p.write_text(xml)
