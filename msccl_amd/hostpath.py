@@ -204,10 +204,51 @@ def all_reduce_host(comms: Sequence[Comm], host_in: Sequence, host_out: Sequence
             c.all_reduce(src[r], dst[r], numel, dtype, op, streams[r])
 
 
+def reduce_scatter_host(comms: Sequence[Comm], host_in: Sequence, host_out: Sequence, dtype: int, op: int = SUM,
+                        streams: Optional[Sequence[int]] = None) -> None:
+    """Zero-copy ReduceScatter of pinned host tensors: host_in[r] holds nranks x recvcount elements,
+    host_out[r] recvcount (rank r's reduced block), as all_reduce_host."""
+    import torch
+    n = len(comms)
+    if not (len(host_in) == len(host_out) == n) or any(t.numel() != host_in[0].numel() for t in host_in):
+        raise ValueError("one host input and output per rank, inputs of one size")
+    recvcount = host_out[0].numel()
+    if host_in[0].numel() != recvcount * n or any(t.numel() != recvcount for t in host_out):
+        raise ValueError("inputs must hold nranks x recvcount elements, outputs recvcount")
+    src = [device_address(t) for t in host_in]
+    dst = [device_address(t) for t in host_out]
+    if streams is None:
+        streams = [torch.cuda.current_stream(c.device).cuda_stream for c in comms]
+    with group():
+        for r, c in enumerate(comms):
+            c.reduce_scatter(src[r], dst[r], recvcount, dtype, op, streams[r])
+
+
+def all_gather_host(comms: Sequence[Comm], host_in: Sequence, host_out: Sequence, dtype: int,
+                    streams: Optional[Sequence[int]] = None) -> None:
+    """Zero-copy AllGather of pinned host tensors: host_in[r] holds sendcount elements, host_out[r]
+    nranks x sendcount, as all_reduce_host."""
+    import torch
+    n = len(comms)
+    if not (len(host_in) == len(host_out) == n):
+        raise ValueError("one host input and output per rank")
+    sendcount = host_in[0].numel()
+    if any(t.numel() != sendcount for t in host_in) or any(t.numel() != sendcount * n for t in host_out):
+        raise ValueError("inputs must hold sendcount elements, outputs nranks x sendcount")
+    src = [device_address(t) for t in host_in]
+    dst = [device_address(t) for t in host_out]
+    if streams is None:
+        streams = [torch.cuda.current_stream(c.device).cuda_stream for c in comms]
+    with group():
+        for r, c in enumerate(comms):
+            c.all_gather(src[r], dst[r], sendcount, dtype, streams[r])
+
+
 def default_chunk_bytes(nbytes: int, chunks: int = 2, floor: int = 1 << 20) -> int:
     """A chunk size for all_reduce_host_staged on nbytes per rank: `chunks` pipeline stages, at least
     `floor` bytes each (each chunk costs ~100 us of cross-stream waits on the copy engines)."""
     return max(floor, (nbytes + chunks - 1) // chunks)
 
 
-__all__: List[str] = ["all_reduce_host", "all_reduce_host_staged", "device_address", "default_chunk_bytes"]
+__all__: List[str] = ["all_reduce_host", "reduce_scatter_host", "all_gather_host", "all_reduce_host_staged",
+                       "device_address", "default_chunk_bytes"]

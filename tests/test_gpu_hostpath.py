@@ -88,3 +88,32 @@ def test_zero_copy_host_allreduce(tmp_path, count, inplace):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_zero_copy_reduce_scatter_and_all_gather(tmp_path):
+    """ReduceScatter then AllGather (C5's pair at 4 ranks, Simple) on pinned host memory: the
+    oracle's values (exact-integer inputs, so any fold order gives the same bits)."""
+    import torch
+    n, rc = 4, (1 << 20) // 4
+    p1, p2 = tmp_path / "rs.xml", tmp_path / "ag.xml"
+    p1.write_text(xmlgen.reduce_scatter_allpairs(n, 2, "Simple", False, 0, 1 << 40, name="rs"))
+    p2.write_text(xmlgen.allgather_allpairs(n, 2, "Simple", False, 0, 1 << 40, name="ag"))
+    os.environ["MSCCL_XML_FILES"] = "%s:%s" % (p1, p2)
+    comms = M.Comm.init_all([0] * n)
+    try:
+        ins = gen_inputs(n, rc * n, 7, 23, mode="exact")
+        hin = [torch.from_numpy(x).pin_memory() for x in ins]
+        hmid = [torch.zeros(rc, dtype=torch.float32).pin_memory() for _ in range(n)]
+        hout = [torch.zeros(rc * n, dtype=torch.float32).pin_memory() for _ in range(n)]
+        hostpath.reduce_scatter_host(comms, hin, hmid, M.FLOAT32, M.SUM)
+        torch.cuda.synchronize()
+        hostpath.all_gather_host(comms, hmid, hout, M.FLOAT32)
+        torch.cuda.synchronize()
+        assert all(c.async_error() == 0 for c in comms)
+        total = np.sum(np.stack([x.astype(np.float64) for x in ins]), axis=0).astype(np.float32)
+        for r in range(n):
+            assert np.array_equal(hmid[r].numpy(), total[r * rc:(r + 1) * rc]), "ReduceScatter rank %d" % r
+            assert np.array_equal(hout[r].numpy(), total), "AllGather rank %d" % r
+    finally:
+        for c in comms:
+            c.destroy()
