@@ -142,7 +142,7 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   if (xmlFiles) loadAlgosFromXmlFiles(xmlFiles, &algos, kMaxChannels, rank, nranks);
   Knobs k = Knobs::fromEnv();
   const bool flat = k.ringFallback && k.treeFlat && nranks <= kMaxReduceFusion;
-  std::vector<int> classes(algos.size(), 0), sendRun(algos.size(), 1);
+  std::vector<int> classes(algos.size(), 0), sendRun(algos.size(), 1), pairAll(algos.size(), 0);
   for (size_t a = 0; a < algos.size(); a++) {
     for (int r = 0; r < nranks; r++) {
       Algorithm ar;
@@ -150,6 +150,13 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
         sendRun[a] = std::max(sendRun[a], algoSendRunOf(ar));
     }
     const Algorithm& g = algos[a];
+    // init.cc: applySplits's pair shape, on every rank (the one-pass merge and the pair kernel)
+    bool shape = k.fuse && !g.path.empty() && g.ngpus == nranks;
+    for (int r = 0; r < nranks && shape; r++) {
+      Algorithm ar;
+      shape = loadAlgoFromXml(g.path.c_str(), &ar, kMaxChannels, r, nranks) == 0 && pairFormOf(ar, fusableTbs(ar)).src >= 0;
+    }
+    pairAll[a] = shape ? 1 : 0;
     if (k.lower && flat && lowerOffered() && g.valid && g.coll == kAllReduce && g.proto == kProtoLL && !g.path.empty() &&
         g.ngpus == nranks) {
       const FoldLowering fl = lowerScheduleFile(g.path, nranks);
@@ -186,13 +193,20 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   Plan p;
   const int res = planCall(pc, c, false, &p);
   if (res != 0) return res;
+  // an MSCCL call of a schedule in pair form on every rank runs the pair kernel on LL when it is one
+  // pass (every full iteration merges into it: up to 64, enqueue.cc: makeWork) and the knob is on
+  const bool pairCall = p.ringColl == 0 && p.algoIndex >= 0 && (size_t)p.algoIndex < pairAll.size() &&
+                        pairAll[p.algoIndex] && p.proto == kProtoLL && k.pairKernel && k.smallKernel &&
+                        (p.nIters <= 1 || (p.nIters <= 64 && p.sizePerChunk % std::max<int64_t>(1, p.chunkSize) == 0));
   const char* kernel = p.ringColl == kTreeFlat ? "fold"
-                       : p.ringColl == kTreeAllReduce ? "tree" : p.ringColl ? "ring" : "interpreter";
+                       : p.ringColl == kTreeAllReduce ? "tree" : p.ringColl ? "ring" : pairCall ? "pair" : "interpreter";
   std::ostringstream o;
   o << "{\"kernel\":\"" << kernel << "\",\"algo\":" << p.algoIndex << ",\"proto\":" << p.proto
     << ",\"lowered\":" << (p.ringColl == kTreeFlat && p.algoIndex >= 0 ? 1 : 0) << ",\"nBytes\":" << p.nBytes
     << ",\"lowerMaxBytes\":" << (k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : defaultLowerMaxBytes(nranks, c.remote))
-    << ",\"simpleBuffBytes\":" << k.buffSizes[kProtoSimple] << ",\"remote\":" << (c.remote ? 1 : 0) << ",\"classes\":[";
+    << ",\"simpleBuffBytes\":" << k.buffSizes[kProtoSimple] << ",\"remote\":" << (c.remote ? 1 : 0)
+    << ",\"pairForm\":" << (p.algoIndex >= 0 && (size_t)p.algoIndex < pairAll.size() ? pairAll[p.algoIndex] : 0)
+    << ",\"classes\":[";
   for (size_t a = 0; a < classes.size(); a++) o << (a ? "," : "") << classes[a];
   o << "]}";
   return putOut(o.str(), out, outLen);

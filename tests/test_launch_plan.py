@@ -117,7 +117,7 @@ def test_pair_form_schedule_keeps_the_pair_kernel(tmp_path, monkeypatch):
     files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(1, "LL")])
     for one_gpu in (True, False):
         got = M.launch_plan_json(files, 0, 2, one_gpu, L.ALLREDUCE, 32, 7, 0, True)
-        assert got["kernel"] == "interpreter" and got["classes"] == [0], got
+        assert got["kernel"] == "pair" and got["classes"] == [0], got
     for env in (("MSCCL_AMD_LOWER_MAX_BYTES", "4096"), ("MSCCL_AMD_PAIR_KERNEL", "0"), ("MSCCL_AMD_FUSE", "0")):
         monkeypatch.setenv(*env)
         got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 32, 7, 0, True)
@@ -126,3 +126,30 @@ def test_pair_form_schedule_keeps_the_pair_kernel(tmp_path, monkeypatch):
     files = _files(tmp_path, [xmlgen.allreduce_allpairs(2, 4, "LL")])
     got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 32, 7, 0, True)
     assert got["kernel"] == "fold", got
+
+
+@pytest.mark.parametrize("nbytes", [128, 8192, 1 << 20, 32 << 20])
+def test_c2_tiers_launch_the_pair_kernel(tmp_path, nbytes):
+    """bench.py's C2 tiers: every size from 128 B to 32 MiB is a pair-form call that runs the pair
+    kernel in one pass, on one GPU and across GPUs; MSCCL_AMD_PAIR_KERNEL=0 leaves the interpreter."""
+    import bench
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    files = ":".join(t[3] for t in tiers)
+    for one_gpu in (True, False):
+        got = M.launch_plan_json(files, 0, 2, one_gpu, L.ALLREDUCE, nbytes // 4, 7, 0, True)
+        assert got["kernel"] == "pair" and got["pairForm"] == 1, (one_gpu, got)
+
+
+def test_pair_kernel_knob_and_non_pair_schedules(tmp_path, monkeypatch):
+    files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(16, "LL")])
+    monkeypatch.setenv("MSCCL_AMD_PAIR_KERNEL", "0")
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 18, 7, 0, True)
+    assert got["kernel"] == "interpreter" and got["pairForm"] == 1, got
+    monkeypatch.delenv("MSCCL_AMD_PAIR_KERNEL")
+    files = _files(tmp_path, [xmlgen.allreduce_allpairs(2, 16, "LL")])
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 20, 7, 0, True)
+    assert got["kernel"] == "interpreter" and got["pairForm"] == 0, got
+    # a call of more than 64 iterations stays on the interpreter (the one-pass merge caps at 64)
+    files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(1, "LL")])
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 24, 7, 0, True)
+    assert got["kernel"] == "interpreter" and got["pairForm"] == 1, got
