@@ -44,10 +44,11 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
  * on one GPU (oneGpu = 1) or spread over GPUs (oneGpu = 0: every rank has peers over xGMI).  The
  * same planning function as the communicator's (plan.cc: planCall) on the same inputs: the
  * schedules, the one-hop lowering and its size limit (co-resident: measured; across GPUs: the
- * link model), the Simple FIFO size, the fallback.  JSON {"kernel": "fold" |
+ * link model), the Simple FIFO size, the fallback, the pair kernel (a one-pass
+ * call of a schedule in pair form on every rank).  JSON {"kernel": "fold" | "pair" |
  * "interpreter" | "ring" | "tree", "algo", "proto", "lowered", "nBytes", "lowerMaxBytes",
- * "simpleBuffBytes", "remote", "classes": [fold orders per algorithm, 0 = not lowered]}.
- * No GPU needed. */
+ * "simpleBuffBytes", "remote", "pairForm", "classes": [fold orders per algorithm, 0 = not
+ * lowered]}.  No GPU needed. */
 int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGpu, int coll, size_t count,
                            int dtype, int redop, int inPlace, char* out, size_t outLen);
 
