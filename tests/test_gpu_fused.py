@@ -312,3 +312,45 @@ def test_c2_tiers_take_the_pair_kernel(nbytes, tmp_path, monkeypatch):
                                   tmpdir=str(tmp_path))
     assert all(l["pair"] == 1 and l["ringColl"] == 0 for l in run_collective.last), run_collective.last
     _check(got, want, "C2 tier %d B" % nbytes)
+
+
+def test_pair_tiers_long_mixed_sequence(tmp_path):
+    """C2's tiers through a long sequence of launches whose sizes jump between the pair kernel
+    (one pass), the small kernel's merged passes (64 MiB, more than 64 iterations) and back, in
+    one communicator pair: the FIFO steps, flags and epochs carried from launch to launch must stay
+    aligned.  Exact-integer inputs; every call is checked against the exact sum."""
+    import torch
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    os.environ["MSCCL_XML_FILES"] = ":".join(t[3] for t in tiers)
+    comms = M.Comm.init_all([0, 0])
+    try:
+        dev = torch.device("cuda:0")
+        maxc = (64 << 20) // 4
+        base = [torch.randint(-4, 5, (maxc,), device=dev, dtype=torch.int32).float() for _ in range(2)]
+        want_full = base[0] + base[1]
+        bufs = [torch.empty(maxc, device=dev) for _ in range(2)]
+        s = torch.cuda.current_stream().cuda_stream
+        sizes = [128, 32 << 20, 4096, 64 << 20, 1 << 20, 8192, 64 << 20, 32 << 20, 128, 16 << 20]
+        kinds = []
+        for rep in range(3):
+            for nb in sizes:
+                cnt = nb // 4
+                for _ in range(4):
+                    for b, x in zip(bufs, base):
+                        b[:cnt].copy_(x[:cnt])
+                    with M.group():
+                        for c, b in zip(comms, bufs):
+                            c.all_reduce(b.data_ptr(), b.data_ptr(), cnt, M.FLOAT32, M.SUM, s)
+                torch.cuda.synchronize()
+                assert all(c.async_error() == 0 for c in comms)
+                for b in bufs:
+                    assert torch.equal(b[:cnt], want_full[:cnt]), "size %d rep %d" % (nb, rep)
+                last = comms[0].info()["last"]
+                kinds.append((nb, last.get("pair", 0), last["small"]))
+        assert (32 << 20, 1, 1) in kinds and (64 << 20, 0, 1) in kinds, kinds
+    finally:
+        for c in comms:
+            c.destroy()
