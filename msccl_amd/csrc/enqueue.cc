@@ -264,14 +264,17 @@ RankWork makeWork(Planned& p) {
     // as many full iterations per call as the bound allows: fewest dependency rounds
     // (C2 32 MiB LL: 348 GB/s with `split` iterations per call, 405 with all 16)
     const int64_t chunk = std::max<int64_t>(1, p.plan.chunkSize);
-    // A schedule in pair form on every rank (transport.cc: pairFormOf; init.cc: algoPairAll) has no
-    // run of sends: every thread block's only send is fused with its receive, one FIFO step ahead
-    // of it, on both ends.  So the bound
-    // does not apply, and every full iteration merges into one pass (the pair kernel).  C2 32 MiB:
-    // one pass instead of two.
+    // A schedule in pair form on every rank (transport.cc: pairFormOf; init.cc: algoPairAll):
+    // every thread block sends one chunk to its peer and receives one from it.  Its run of sends
+    // may fill the whole FIFO (kLLFifoSlots, not kMaxRunSlots): both ends' runs fit at once even
+    // when a rank runs the general kernel, which does not fuse and sends the run before receiving
+    // (a run past the FIFO deadlocks against the peer's, profiles/r05am_pair_merge.txt), and a
+    // rank's next launch only waits for the peer to drain this one.  C2 32 MiB: 64 iterations of
+    // 8 slots per workgroup, one pass on the pair kernel instead of two.
     const bool pairForm = p.plan.proto == kProtoLL && (size_t)p.plan.algoIndex < comm->algoPairAll.size() &&
                           comm->algoPairAll[p.plan.algoIndex];
-    const int64_t fit = pairForm ? 64 : std::max<int64_t>(1, w.maxOpElems / (chunk * sendRun));
+    const int64_t runElems = pairForm ? w.maxOpElems / kMaxRunSlots * kLLFifoSlots : w.maxOpElems;
+    const int64_t fit = std::max<int64_t>(1, runElems / (chunk * sendRun));
     merge = (int)std::min<int64_t>(envMerge > 0 ? envMerge : fit, fit);  // MSCCL_AMD_MERGE only lowers it
     // a merged iteration stays within 1 GiB, far inside a buffer descriptor's 2 GiB reach
     const int64_t reach = std::max<int64_t>(1, (1ll << 30) / (chunk * refTypeSize(p.plan.dtype)));

@@ -354,3 +354,41 @@ def test_pair_tiers_long_mixed_sequence(tmp_path):
     finally:
         for c in comms:
             c.destroy()
+
+
+def test_pair_merge_bound_with_small_fifo_and_general_peer(tmp_path):
+    """A pair-form call's merged run of sends stays within the FIFO whatever its slot size: with
+    NCCL_LL_BUFFSIZE=256 KiB (32-KiB slots) a 32 MiB call is 16 slots per workgroup, so it runs as
+    two passes of 8; rank 1 runs the general kernel, which sends its whole run before receiving
+    (a one-pass cut would deadlock against rank 0's pair of runs).  The oracle's values."""
+    import torch.multiprocessing as mp
+    from oracle import plan as P, sim as S
+    world, count = 2, 1 << 23
+    xml = xmlgen.allreduce_pair_oneshot(16, "LL")
+    p = tmp_path / "pair16.xml"
+    p.write_text(xml)
+    small_fifo = {"NCCL_LL_BUFFSIZE": str(256 << 10)}
+    envs = [dict(small_fifo), dict(small_fifo, MSCCL_AMD_SMALL_KERNEL="0")]
+    ctx = mp.get_context("spawn")
+    q_in, q_out = ctx.Queue(), ctx.Queue()
+    ps = [ctx.Process(target=_pair_mixed_proc, args=(r, world, str(p), count, envs[r], q_in, q_out))
+          for r in range(world)]
+    for pr in ps:
+        pr.start()
+    res = {}
+    for _ in range(world):
+        r, err, small, pair, out = q_out.get(timeout=300)
+        res[r] = (err, small, pair, out)
+    for pr in ps:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    assert res[1][1] == 0, res[1][:3]
+    algos = [L.parse_xml(xml, r, world) for r in range(world)]
+    call = P.Call(L.ALLREDUCE, count, 7, 0, world, 0, True)
+    plan = P.make_plan([algos[0]], call, 0)
+    ins = gen_inputs(world, count, 7, 9)
+    for _ in range(3):
+        ins, _st = S.run(algos, plan, ins, [None] * world, L.ALLREDUCE, True)
+    for r in range(world):
+        assert res[r][0] == 0
+        assert np.array_equal(res[r][3].view(np.uint32), np.asarray(ins[r]).view(np.uint32))
