@@ -194,7 +194,9 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   const int res = planCall(pc, c, false, &p);
   if (res != 0) return res;
   // an MSCCL call of a schedule in pair form on every rank runs the pair kernel on LL when it is one
-  // pass (every full iteration merges into it: up to 64, enqueue.cc: makeWork) and the knob is on
+  // pass and the knob is on (enqueue.cc: makeWork merges a pair-form call's iterations while a
+  // workgroup's sends fit the FIFO: 64 iterations at the default LL FIFO and split 8, the bound
+  // used here)
   const bool pairCall = p.ringColl == 0 && p.algoIndex >= 0 && (size_t)p.algoIndex < pairAll.size() &&
                         pairAll[p.algoIndex] && p.proto == kProtoLL && k.pairKernel && k.smallKernel &&
                         (p.nIters <= 1 || (p.nIters <= 64 && p.sizePerChunk % std::max<int64_t>(1, p.chunkSize) == 0));
