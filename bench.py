@@ -151,6 +151,40 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only:
     return int(round(hbm)), int(round(wire))
 
 
+KERNEL_NAMES = {0: "mscclKernel", 1: "mscclSmallKernel", 2: "mscclFoldKernel (lowered)",
+                3: "mscclPairKernel", 4: "mscclTwoPhaseKernel (lowered)"}
+
+
+def kernel_name(last: dict) -> str:
+    """The kernel a communicator's last launch ran (comm info "last", enqueue.cc: launchGroup)."""
+    k = last.get("kernel", -1)
+    if k == 3 and last.get("ringColl") == 5:
+        return "mscclPairKernel (lowered)"
+    if k == 1 and last.get("set") == 1:
+        return "mscclSmallKernel<exchange set>"
+    return KERNEL_NAMES.get(k, "mscclKernel")
+
+
+def lowered_bytes(last: dict, n: int, nbytes: int):
+    """(HBM bytes, wire bytes, payload-only HBM bytes) of one rank's lowered launch (LL lines: 16 B
+    per 8-B payload), or None when the launch ran the schedule as written (schedule_bytes then):
+      fold (kernel 2): the input read once, lines to and from each of the n - 1 peers, the result;
+      lowered pair (kernel 3 on the flat connections): S read, 2 S of lines out, 2 S in, S written;
+      two-phase (kernel 4): per (n - 1)/n S of peer-owned data: read, lines out (A), lines in and
+        the owner's result lines in (C), written; per S/n owned: read, the peers' lines in (B),
+        written, result lines out: (10 (n - 1) + 2) / n S (9 S at 8 ranks, 6 S at 2)."""
+    k = last.get("kernel", -1)
+    if k == 2:
+        return (int(2 * nbytes + 2 * 2.0 * (n - 1) * nbytes), int(2.0 * (n - 1) * nbytes),
+                int(2 * nbytes + 2 * (n - 1) * nbytes))
+    if k == 3 and last.get("ringColl") == 5:
+        return 6 * nbytes, 2 * nbytes, 4 * nbytes
+    if k == 4:
+        return (int(round((10 * (n - 1) + 2) * nbytes / n)), int(round(4 * (n - 1) * nbytes / n)),
+                int(round((6 * (n - 1) + 2) * nbytes / n)))
+    return None
+
+
 def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None, remote: bool = False):
     """All-pairs schedules in size tiers, as a user registers several msccl-tools XMLs with
     minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
@@ -535,7 +569,25 @@ def run_secondary(name: str, xml_text: str, n: int, nbytes: int, dt: int, a, mul
             t, ev_ms = float(tt[0]), float(tt[1])
         if any(c.async_error() != 0 for c in comms):
             raise RuntimeError("kernel reported an error (timeout/abort)")
-        small = comms[0].info()["last"].get("small", 0) == 1
+        info = comms[0].info()
+        last = info["last"]
+        # the launch's algorithmic bytes (the bytes model of what ran: the schedule as written, or
+        # its lowered form) and the memory-side / payload fractions of the 8 TB/s peak, as the
+        # headline's roofline computes them
+        low = lowered_bytes(last, n, nbytes)
+        if low is not None:
+            hbm, _, payload = low
+        else:
+            algo = M.algo_json(pth, rank if multi else 0, n)
+            fz = set(info.get("algoFuse", [[]])[0]) if last.get("small", 0) == 1 else ()
+            size_per = cnt // algo["nchunksperloop"]
+            hbm, _ = schedule_bytes(algo, size_per, ts, 0, fused=fz)
+            payload, _ = schedule_bytes(algo, size_per, ts, 0, payload_only=True, fused=fz)
+        on_gpu = 1 if multi else n
+        kern_s = ev_ms / 1e3
+        roof = {"algorithmic_bytes": hbm * on_gpu, "payload_bytes": payload * on_gpu,
+                "memside_frac": round(hbm * on_gpu / kern_s / 1e9 / HBM_PEAK_GBS, 4),
+                "payload_frac": round(payload * on_gpu / kern_s / 1e9 / HBM_PEAK_GBS, 4)}
         j = torch.arange(cnt, device=dev, dtype=torch.int64)
         pat = [((j * 7 + r * 3 + (j >> 5)) % 9 - 4).to(torch.float32) for r in range(n)]
         for r, b in zip(ranks, bufs):
@@ -552,7 +604,7 @@ def run_secondary(name: str, xml_text: str, n: int, nbytes: int, dt: int, a, mul
         return {"ranks": n, "bytes": nbytes, "dtype": {M.FLOAT32: "f32", M.FLOAT16: "f16", M.BFLOAT16: "bf16"}[dt],
                 "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
                 "busbw": round(nbytes / t * 2 * (n - 1) / n / 1e9, 3), "verified": good, "steps": k,
-                "kernel": "mscclSmallKernel" if small else "mscclKernel"}
+                "kernel": kernel_name(last), "lowered": low is not None, **roof}
     finally:
         for c in comms:
             c.destroy()
@@ -798,14 +850,10 @@ def main():
         # applies to sizes whose launches ran there (comm info "last": the kernel of the last launch)
         last = comms[0].info()["last"]
         small = last.get("small", 0) == 1
-        lowered = last.get("small", 0) == 2   # the one-hop fold (msccl_amd/csrc/lower.cc)
         fz = fused.get(tier[3], ()) if small else ()
-        if lowered:
-            # the fold kernel: the input read once, LL lines to and from each of the n-1 peers,
-            # the result written
-            hbm = int(2 * nbytes + 2 * 2.0 * (n - 1) * nbytes)
-            wire = int(2.0 * (n - 1) * nbytes)
-            payload = int(2 * nbytes + 2 * (n - 1) * nbytes)
+        low = lowered_bytes(last, n, nbytes)   # a lowered launch (msccl_amd/csrc/lower.cc)
+        if low is not None:
+            hbm, wire, payload = low
         else:
             hbm, wire = schedule_bytes(algo, size_per, ts, proto_id, fused=fz)
             payload, _ = schedule_bytes(algo, size_per, ts, proto_id, payload_only=True, fused=fz)
@@ -813,10 +861,7 @@ def main():
         verified.append(ok)
         results.append({"bytes": nbytes, "ms": round(t * 1e3, 5), "kernel_ms": round(ev_ms, 5),
                         "payload_bytes_per_rank": payload, "verified": ok, "small": small,
-                        "kernel": ("mscclFoldKernel (lowered)" if lowered else
-                                   "mscclPairKernel" if last.get("pair") == 1 else
-                                   "mscclSmallKernel%s" % ("<exchange set>" if last.get("set") == 1 else "")
-                                   if small else "mscclKernel"),
+                        "kernel": kernel_name(last), "lowered": low is not None,
                         "fused": bool(fz), "tier": tier[4],
                          "algbw": round(algbw, 3), "busbw": round(bus, 3),
                          "hbm_bytes_per_rank": hbm, "wire_bytes_per_rank": wire})

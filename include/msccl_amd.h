@@ -63,6 +63,12 @@ int mscclAmdBootstrapAllgather(const ncclUniqueId* id, int rank, int nranks, con
 /* Number of thread blocks a launch of algorithm `algoIndex` uses on this rank. */
 int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex);
 
+/* Host-only build check (no GPU needed): the name of the first element type whose kernel object
+   was compiled with another RankWork layout than this library's host code ("float32", ...), or
+   NULL when every object agrees.  Communicator setup refuses such a library (ncclInternalError);
+   tools/varbuild.sh runs this right after linking a measurement variant, before any GPU run. */
+const char* mscclAmdKernelLayoutMismatch(void);
+
 /* Device event trace (NPKit-style, the reference's src/include/npkit/): enabled per communicator
  * with MSCCL_AMD_TRACE=1 at init.  Each workgroup slot (tb * maxSplit + sub) records up to
  * MSCCL_AMD_TRACE_EVENTS 16-byte events of its most recent launch:

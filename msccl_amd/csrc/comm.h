@@ -76,6 +76,9 @@ struct ncclComm {
   struct FoldProgram {
     std::vector<int> chunkClass;            // class of every chunk (lower.h)
     std::vector<std::vector<int>> order;    // this rank's fold order (ranks) per class; empty: not lowered
+    // the two-phase form (lower.h: FoldLowering::twoPhase, agreed by every rank at init): the
+    // owner of every chunk; empty when the schedule has none
+    std::vector<int> owner;
   };
   std::vector<FoldProgram> algoFold;
   std::vector<int> algoSet;  // per algorithm: the small kernel's transfer set (transport.cc: algoUpload)
@@ -93,6 +96,7 @@ struct ncclComm {
   bool anyRemote = false;          // some peer runs on another GPU (xGMI): no LL128 unless allowed
   std::vector<int> algoSplit;      // workgroups per XML thread block, per algorithm (same on all ranks)
   std::vector<int> algoSplitBase;  // the split of the default budget (algoSplit is wider for 2 co-resident LL ranks)
+  std::vector<int> algoMaxBlocks;  // per algorithm: the most thread blocks of any rank's program (same on all ranks)
   std::vector<int> algoSendRun;    // per algorithm: longest run of send chunks before a receive, max over
                                    // every rank's program (same on all ranks)
   std::vector<std::vector<msccl::FuseCandidate>> algoFuse;  // per algorithm: thread blocks running fused
@@ -100,6 +104,7 @@ struct ncclComm {
   int maxSplit = 1;                // sub-connections per (channel, peer)
   int coResident = 1;              // ranks of this communicator on this rank's GPU
   std::vector<int> foldClasses;    // per algorithm: algoFold's class count (0: not lowered)
+  std::vector<int> foldTwoPhase;   // per algorithm: algoFold has the two-phase form (owner table)
   msccl::PlanContext planCtx;      // what planCall reads (set at the end of init: commFinish)
 
   // transport
@@ -113,8 +118,11 @@ struct ncclComm {
   msccl::DevRecvConn* ringRecv = nullptr;
   msccl::DevSendConn* treeSend = nullptr;              // tree fallback connections [2 * kRingChannels]
   msccl::DevRecvConn* treeRecv = nullptr;
-  msccl::DevSendConn* flatSend = nullptr;              // flat tree connections [nRanks] (tb 0 has none)
+  msccl::DevSendConn* flatSend = nullptr;              // flat tree connections [nRanks][flatSubs] (tb 0 has none)
   msccl::DevRecvConn* flatRecv = nullptr;
+  // sub-connections per flat connection: kFlatSubs, or the lowered large calls' workgroups per
+  // rank when a schedule runs them (init.cc: applySplits; the same on every rank)
+  int flatSubs = msccl::kFlatSubs;
   int llSlotLines = 0, simpleSlotBytes = 0;
   int buffSizes[3] = {0, 0, 0};
 
@@ -152,6 +160,7 @@ struct ncclComm {
     int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0, small = 0;
     int set = 0;  // the small kernel's transfer set (devcomm.h: kSetAll / kSetExchange)
     int pair = 0;  // the exchange ran in the pair kernel (mscclPairKernel)
+    int kernel = -1;  // 0 mscclKernel, 1 mscclSmallKernel, 2 mscclFoldKernel, 3 mscclPairKernel, 4 mscclTwoPhaseKernel
   } last;
 
   // user reduction ops (ncclRedOpCreatePreMulSum, enqueue.cc:1529-1580): a free list as in the

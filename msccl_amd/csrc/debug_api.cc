@@ -78,7 +78,15 @@ int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen)
     }
     o << "],\"chunkClass\":[";
     for (size_t c = 0; c < fl.chunkClass.size(); c++) o << (c ? "," : "") << fl.chunkClass[c];
-    o << "]";
+    // the two-phase form: every chunk's owner (lower.h), or why there is none
+    o << "],\"twoPhase\":" << (fl.twoPhase ? 1 : 0);
+    if (fl.twoPhase) {
+      o << ",\"owner\":[";
+      for (size_t c = 0; c < fl.owner.size(); c++) o << (c ? "," : "") << fl.owner[c];
+      o << "]";
+    } else {
+      o << ",\"whyNotTwoPhase\":\"" << fl.whyNotTwoPhase << "\"";
+    }
   } else {
     o << ",\"why\":\"" << fl.why << "\"";
   }
@@ -142,7 +150,8 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   if (xmlFiles) loadAlgosFromXmlFiles(xmlFiles, &algos, kMaxChannels, rank, nranks);
   Knobs k = Knobs::fromEnv();
   const bool flat = k.ringFallback && k.treeFlat && nranks <= kMaxReduceFusion;
-  std::vector<int> classes(algos.size(), 0), sendRun(algos.size(), 1), pairAll(algos.size(), 0);
+  std::vector<int> classes(algos.size(), 0), sendRun(algos.size(), 1), pairAll(algos.size(), 0),
+      twoPhase(algos.size(), 0);
   for (size_t a = 0; a < algos.size(); a++) {
     for (int r = 0; r < nranks; r++) {
       Algorithm ar;
@@ -161,6 +170,7 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
         g.ngpus == nranks) {
       const FoldLowering fl = lowerScheduleFile(g.path, nranks);
       if (fl.ok) classes[a] = (int)fl.order.size();
+      if (fl.ok && fl.twoPhase) twoPhase[a] = 1;
       // init.cc: applySplits keeps a schedule every rank runs with the pair kernel off the fold
       bool pairEverywhere = k.lowerMaxBytes < 0 && k.fuse && k.pairKernel;
       for (int r = 0; r < nranks && pairEverywhere; r++) {
@@ -178,6 +188,7 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   pc.regs = &regs;
   pc.knobs = &k;
   pc.foldClasses = &classes;
+  pc.foldTwoPhase = &twoPhase;
   pc.flat = flat;
   pc.ringFallback = k.ringFallback != 0;
   pc.scratchSize = (size_t)-1;  // uncapped (MSCCL_AMD_MAX_SCRATCH is not modelled here)
@@ -200,7 +211,9 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   const bool pairCall = p.ringColl == 0 && p.algoIndex >= 0 && (size_t)p.algoIndex < pairAll.size() &&
                         pairAll[p.algoIndex] && p.proto == kProtoLL && k.pairKernel && k.smallKernel &&
                         (p.nIters <= 1 || (p.nIters <= 64 && p.sizePerChunk % std::max<int64_t>(1, p.chunkSize) == 0));
-  const char* kernel = p.ringColl == kTreeFlat ? "fold"
+  const char* kernel = p.ringColl == kTreeFlat ? (p.lowerMode == kLowerPair       ? "pair"
+                                                  : p.lowerMode == kLowerTwoPhase ? "twophase"
+                                                                                  : "fold")
                        : p.ringColl == kTreeAllReduce ? "tree" : p.ringColl ? "ring" : pairCall ? "pair" : "interpreter";
   std::ostringstream o;
   o << "{\"kernel\":\"" << kernel << "\",\"algo\":" << p.algoIndex << ",\"proto\":" << p.proto
@@ -243,7 +256,8 @@ int mscclAmdCommInfo(ncclComm_t comm, char* out, size_t outLen) {
   const auto& L = comm->last;
   o << "],\"last\":{\"algo\":" << L.algo << ",\"proto\":" << L.proto << ",\"split\":" << L.split
     << ",\"merge\":" << L.merge << ",\"ringColl\":" << L.ringColl << ",\"ringChannels\":" << L.ringChannels
-    << ",\"blocks\":" << L.blocks << ",\"small\":" << L.small << ",\"set\":" << L.set << ",\"pair\":" << L.pair << "}}";
+    << ",\"blocks\":" << L.blocks << ",\"small\":" << L.small << ",\"set\":" << L.set << ",\"pair\":" << L.pair
+    << ",\"kernel\":" << L.kernel << "},\"flatSubs\":" << comm->flatSubs << "}";
   return putOut(o.str(), out, outLen);
 }
 
@@ -264,6 +278,8 @@ int mscclAmdSetEnvFile(const char* path) {
   if (path == nullptr) return ncclInvalidArgument;
   return setEnvFile(path) ? ncclSuccess : ncclSystemError;
 }
+
+const char* mscclAmdKernelLayoutMismatch(void) { return kernelLayoutMismatch(); }
 
 int mscclAmdAlgoBlocks(ncclComm_t comm, int algoIndex) {
   if (!commValid(comm) || algoIndex < 0 || algoIndex >= (int)comm->algos.size()) return -1;

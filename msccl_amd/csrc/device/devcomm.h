@@ -40,6 +40,10 @@ constexpr int kMaxFoldPeers = 15;      // flat tree fold: peers of one rank (MSC
 // 12.5 (lanes walking 4 packs, each poll waiting for the last), 64 KiB 15.6 against 11.3, small
 // calls unchanged (profiles/r04t_lat.txt).  LL FIFOs only: 8 MiB per peer
 constexpr int kFlatSubs = 16;
+// Lowered large calls (the pair kernel on the flat connections for 2 ranks, the two-phase fold
+// for more: lower.h) run up to this many workgroups per rank, one sub-connection each (the
+// workgroup count travels in RankWork::split, a byte)
+constexpr int kMaxFlatSubs = 128;
 constexpr int kFoldPacksPerWg = 512;   // flat tree: a fold workgroup per 512 packs (8 KiB) of the call
 constexpr int kMaxFoldClasses = 16;    // lowered schedules (lower.cc): fold orders per schedule
 constexpr int kMaxFoldChunks = 1024;   // lowered schedules with several orders: chunks per loop
@@ -225,14 +229,33 @@ struct RankWork {
   int32_t redOpArgIsPtr;        // redOpArg is a device address of the scalar (ncclScalarDevice)
   uint64_t redOpArg;            // PreMulSum scale bits / SumPostDiv divisor (ncclDevRedOpFull::scalarArg)
   NpkitLog* npkit;              // MSCCL_AMD_NPKIT (null = off)
+  // the two-phase fold (mscclTwoPhaseKernel): the 16-B packs each rank owns (chunks per rank x
+  // foldChunkPacks), and the division by foldChunkPacks as a multiply-high and two shifts (exact
+  // for every 32-bit dividend: divMagic of Granlund and Montgomery, computed by the host)
+  uint32_t tpOwnedPacks;
+  uint32_t tpMagic;
+  uint8_t tpSh1, tpSh2;
+  uint16_t tpStepPacks;         // packs per FIFO step (at most a slot's): the FIFO footprint in flight
+#ifdef MSCCL_RANKWORK_TEST_PAD
+  // a deliberate layout split (tools/varbuild.sh's guard test): a kernel object built with this
+  // define has a larger RankWork, so it reads every rank's entry after the first of the launch
+  // argument block (LaunchArgsN::w) at another offset than the host wrote it
+  int32_t testPad;
+#endif
 };
 
 // Layout stamp of RankWork: every kernel object records the one it was compiled with (kernels.h)
 // and communicator setup refuses a library whose objects disagree with the host's
 // (dispatch.cc: kernelLayoutMismatch) -- a kernel object left over from before a RankWork change
 // reads its arguments at the wrong offsets, an illegal memory access rather than an error code.
-constexpr uint32_t kWorkLayout = (uint32_t)sizeof(RankWork) << 20 ^ (uint32_t)offsetof(RankWork, maxOpElems) << 10 ^
-                                 (uint32_t)offsetof(RankWork, npkit);
+// The stamp folds the size and the offsets of fields spread over the whole struct, so a field added,
+// removed or resized anywhere (a -D flag given to one object only, a stale object) changes it.
+constexpr uint32_t layoutMix(uint32_t h, uint32_t v) { return (h ^ v) * 16777619u; }  // FNV-1a step
+constexpr uint32_t kWorkLayout =
+    layoutMix(layoutMix(layoutMix(layoutMix(layoutMix(layoutMix(layoutMix(layoutMix(layoutMix(2166136261u,
+    (uint32_t)sizeof(RankWork)), (uint32_t)offsetof(RankWork, tbStride)), (uint32_t)offsetof(RankWork, sizePerChunk)),
+    (uint32_t)offsetof(RankWork, blockBase)), (uint32_t)offsetof(RankWork, pairSrc)), (uint32_t)offsetof(RankWork, maxOpElems)),
+    (uint32_t)offsetof(RankWork, ringSize)), (uint32_t)offsetof(RankWork, npkit)), (uint32_t)offsetof(RankWork, tpStepPacks));
 
 template <int R>
 struct LaunchArgsN {
@@ -270,6 +293,9 @@ LaunchFn getFoldLaunchFn(int dtype, int redop);   // mscclFoldKernel (the flat t
 // thread block: one fused s + rrc of one chunk at an affine chunk index, no dependency) in one
 // pass: no program image, the first FIFO step's source loaded with the connection records.
 LaunchFn getPairLaunchFn(int dtype, int redop);
+// The two-phase fold (mscclTwoPhaseKernel, interpreter.h: runTwoPhase): a lowered schedule's
+// large calls, LL, Sum..Min
+LaunchFn getTwoPhaseLaunchFn(int dtype, int redop);
 // the name of the first type whose kernel object was built with another RankWork layout, or null
 const char* kernelLayoutMismatch();
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):

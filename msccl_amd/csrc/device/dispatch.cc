@@ -3,7 +3,7 @@
 
 namespace msccl {
 #define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[2][4]; extern LaunchFn N##_fold[4]; \
-  extern LaunchFn N##_pair[4]; extern OneRankFn N##_one; extern const uint32_t N##_layout;
+  extern LaunchFn N##_pair[4]; extern LaunchFn N##_two[4]; extern OneRankFn N##_one; extern const uint32_t N##_layout;
 MSCCL_DECL(gLaunch_i8)
 MSCCL_DECL(gLaunch_u8)
 MSCCL_DECL(gLaunch_i32)
@@ -45,6 +45,14 @@ LaunchFn getFoldLaunchFn(int dtype, int devOp) {
 LaunchFn getPairLaunchFn(int dtype, int devOp) {
   LaunchFn* tabs[10] = {gLaunch_i8_pair, gLaunch_u8_pair, gLaunch_i32_pair, gLaunch_u32_pair, gLaunch_i64_pair,
                         gLaunch_u64_pair, gLaunch_f16_pair, gLaunch_f32_pair, gLaunch_f64_pair, gLaunch_bf16_pair};
+  if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
+  return tabs[dtype][devOp];
+}
+
+// the two-phase fold (mscclTwoPhaseKernel): LL, devOp Sum..Min
+LaunchFn getTwoPhaseLaunchFn(int dtype, int devOp) {
+  LaunchFn* tabs[10] = {gLaunch_i8_two, gLaunch_u8_two, gLaunch_i32_two, gLaunch_u32_two, gLaunch_i64_two,
+                        gLaunch_u64_two, gLaunch_f16_two, gLaunch_f32_two, gLaunch_f64_two, gLaunch_bf16_two};
   if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
   return tabs[dtype][devOp];
 }

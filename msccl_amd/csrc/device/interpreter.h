@@ -56,6 +56,7 @@ struct alignas(16) FoldShared {
     const LLLine* in;   // recv slot of this step
     uint32_t sflag, rflag;
   } fold[kMaxFoldPeers];
+  Peer fold2[kMaxFoldPeers];  // the two-phase fold: the second slot of the step (the owners' results)
   uint8_t perm[kMaxFoldPeers + 1];  // peer record of each fold position (the own input skipped)
   // a lowered schedule folding its chunks in several orders (lower.cc: classes): per class the
   // peer record of each fold position and the position of the own input; the class of each chunk
@@ -1680,6 +1681,310 @@ struct Interp {
     }
   }
 
+  // ---------------------------------------------------------------- the two-phase fold
+  // A lowered schedule's large call (lower.h: FoldLowering::twoPhase; plan.cc: lowerToFoldPlan;
+  // the msccl-tools two-phase all-pairs, RCCL's allreduce-allpairs files): the schedule's values
+  // without its scratch.  The schedule moves chunk c of every rank's input into owner[c]'s scratch
+  // (`s`, `r`), the owner folds the n copies with `re` (acc = own, acc = fn(acc, s_i) in its
+  // reduction order, prims_ll.h:347-362) and sends the result to every peer (`s`, `r`), i.e. per
+  // element 7.5 S (2 ranks) / 11.6 S (8 ranks) HBM bytes per rank.  Here the owner folds straight
+  // from the FIFO lines, in the same order, and sends the result on in the same pass: 6 S / 9 S.
+  //
+  // Every rank owns K chunks of Q packs (transfer 5 of the image lists them per peer record, then
+  // this rank's); owned pack m of rank q is pack m % Q of its chunk m / Q (lists[q][m / Q]).  All
+  // ranks deal m over their workgroups the same way (RankWork::foldPacksPerWg): workgroup wg owns
+  // m in [p0, p0 + npk) of every rank's set and talks to workgroup wg of every peer over flat
+  // sub-connection wg.  Per FIFO step (slotPacks of those m), every peer connection carries two
+  // slots: (A) this rank's packs of the peer's set, (B) the owner's results.  For every step j a
+  // workgroup
+  //   A(j): sends its input's packs of every peer's set to that peer (slot A);
+  //   B(j): polls every peer's slot-A lines of its own set, folds them with its own input in its
+  //      chunk's class order (the order lower.cc read off the schedule), stores the result and
+  //      sends it to every peer (slot B);
+  //   C(j): polls every peer's slot-B lines and stores each owner's result in its place.
+  // A lane reads an input pack (A, B) before it writes that pack (B, C), and the steps in flight
+  // at once own disjoint packs: in-place calls are safe.  The three phases are software-pipelined
+  // over the steps (below); no workgroup waits on a peer's step the peer has not reached, so the
+  // loop cannot deadlock.
+  __device__ __forceinline__ uint32_t divQ(uint32_t m, uint32_t magic, int sh1, int sh2) const {
+    const uint32_t t = __umulhi(m, magic);
+    return (t + ((m - t) >> sh1)) >> sh2;
+  }
+  __device__ __forceinline__ void runTwoPhase(const RankWork& w, int wg, FoldShared* fs) {
+    tid = threadIdx.x;
+    comm = w.comm;
+    timeoutTicks = w.timeoutTicks;
+    llFlagMask = w.llFlagMask;
+    llCleanMask = w.llCleanMask;
+    redArg = 0;
+    trace = nullptr;
+    nkBuf = nullptr;
+    scG = nullptr;
+    rcG = nullptr;
+    const int np = w.foldPeers;
+    const int n = (int)w.sizePerChunk;  // elements of the whole buffer
+    const int wgs = w.split, base = w.foldPacksPerWg, connSplit = w.connSplit, tbStride = w.tbStride;
+    const int M = (int)w.tpOwnedPacks, Q = w.foldChunkPacks;
+    const uint32_t magic = w.tpMagic;
+    const int sh1 = w.tpSh1, sh2 = w.tpSh2;
+    const char* const images = w.images;
+    DevSendConn* const sendG = w.send;
+    DevRecvConn* const recvG = w.recv;
+    uint64_t* const epochs = w.epochs;
+    const void* const sendbuff = w.sendbuff;
+    void* const recvbuff = w.recvbuff;
+    pinArgs(np, n, wgs, base, connSplit, tbStride, images, sendG, recvG, epochs, sendbuff, recvbuff);
+    constexpr int G = 8;  // peers per wait / per batch of loads
+    const int rem = M - base * wgs;
+    const int p0 = wg * base + min(wg, rem);
+    const int npk = base + (wg < rem ? 1 : 0);
+    const __amdgpu_buffer_rsrc_t srs = makeRsrc(sendbuff), drs = makeRsrc(recvbuff);
+    const bool vec = aligned16(sendbuff) && aligned16(recvbuff);
+    {
+      // one round trip: the image (orders, classes, owner lists), every peer's records, the epoch
+      const u32x4* gimg = (const u32x4*)images;
+      const int nU = tbStride >> 4;
+      for (int i = tid; i < nU; i += kNT) sh->img[i] = gimg[i];
+      if (tid >= 64 && tid < 64 + 4 * np) {
+        const int k = (tid - 64) >> 2, j = (tid - 64) & 3;
+        ((u32x4*)&fs->foldSend[k])[j] = ((const u32x4*)(sendG + (size_t)(k + 1) * connSplit + wg))[j];
+      }
+      if (tid >= 192 && tid < 192 + 4 * np) {
+        const int k = (tid - 192) >> 2, j = (tid - 192) & 3;
+        ((u32x4*)&fs->foldRecv[k])[j] = ((const u32x4*)(recvG + (size_t)(k + 1) * connSplit + wg))[j];
+      }
+      if (tid == 128) {
+        sh->aborted = 0;
+        sh->epoch = atomicLoadAgent(epochs + wg);
+      }
+    }
+    __syncthreads();
+    const uint64_t workIndex = uni(sh->epoch);
+    DevTbHeader hd;
+    {
+      u32x4 raw = sh->img[0];
+      raw = (u32x4){uni(raw.x), uni(raw.y), uni(raw.z), uni(raw.w)};
+      __builtin_memcpy(&hd, &raw, sizeof(hd));
+    }
+    const DevTransfer* tr0 = (const DevTransfer*)&sh->img[1];
+    const int16_t* reds = (const int16_t*)(tr0 + hd.nsteps) + 2 * hd.ndeps;
+    const int nfold = loadTransfer(tr0).numReds;
+    const DevTransfer t3 = loadTransfer(tr0 + 3), t4 = loadTransfer(tr0 + 4), t5 = loadTransfer(tr0 + 5);
+    {
+      const int16_t* co = reds + t3.redPtr;
+      for (int i = tid; i < t3.srcoff; i += kNT) {  // one lane per class: its peer records in fold order
+        int q = 0;
+        for (int j = 0; j < nfold; j++) {
+          const int b = co[i * nfold + j];
+          if (b < 0) fs->cown[i] = (uint8_t)q;
+          else fs->cperm[i][q++] = (uint8_t)(b - 1);
+        }
+      }
+      const int16_t* cc = reds + t4.redPtr;
+      for (int i = tid; i < t4.srcoff; i += kNT) fs->chunkClass[i] = (uint8_t)cc[i];
+    }
+    const int16_t* lists = reds + t5.redPtr;  // [peer record k (np: this rank)][K] owned chunks
+    const int K = t5.srcoff;
+    const int slotLines = uni(fs->foldRecv[0].llSlotLines);
+    // packs per step: at most a slot's (RankWork::tpStepPacks; smaller steps keep the FIFO lines in
+    // flight within the MALL)
+    const int slotPacks = min(slotLines / 2, (int)w.tpStepPacks);
+    // Software pipeline: iteration i sends A(i), folds B(i - 1) and stores C(i - 2), so each of
+    // them needs only what the peers did one iteration earlier (A(i - 1), B(i - 2)): a workgroup
+    // waits only for a peer a whole iteration behind.  Slots per connection: A(j) at base + 2j,
+    // B(j) at base + 2j + 1.  After iteration i a receiver has consumed A(0 .. i - 1) and
+    // B(0 .. i - 2): it frees the consumed prefix of its FIFO.  The sender of A(i) needs the
+    // peer's head at 2i - 7 or more: at most three iterations ahead of its slowest peer.
+    const int nsteps = (npk + slotPacks - 1) / slotPacks;
+    auto nsOf = [&](int j) { return min(slotPacks, npk - j * slotPacks); };
+    // this lane's pack q of step j: its chunk index j in every owner's list and position in it
+    auto packOf = [&](int j, int q, int& jj, int& pos) __attribute__((always_inline)) {
+      const uint32_t m = (uint32_t)(p0 + j * slotPacks + q);
+      jj = (int)divQ(m, magic, sh1, sh2);
+      pos = (int)m - jj * Q;
+    };
+    for (int i = 0; i <= nsteps + 1; i++) {
+      const bool doA = i < nsteps, doB = i >= 1 && i <= nsteps, doC = i >= 2;
+      if (tid < np) {
+        // lane k: credit for the highest slot this iteration writes (A(i) at 2i, else B(i - 1) at
+        // 2i - 1), and the four slots of the iteration
+        DevSendConn& c = fs->foldSend[tid];
+        const uint64_t b = c.step;  // base: the connection's step at launch start (advanced at the end)
+        const uint64_t top = doA ? b + 2 * i + 1 : doB ? b + 2 * i : 0;
+        if (top > 0 && c.headSeen + kLLFifoSlots < top) {
+          Spin spins;
+          uint64_t h;
+          while ((h = atomicLoadSys(c.head)) + kLLFifoSlots < top)
+            if (spinAbort(spins)) break;
+          c.headSeen = h;
+        }
+        const uint64_t sa = b + 2 * i, sb = b + 2 * i - 1;  // A(i), B(i - 1)
+        fs->fold[tid].out = c.ll + (sa % kLLFifoSlots) * (uint64_t)c.llSlotLines;
+        fs->fold[tid].sflag = (uint32_t)(sa + 1) & llFlagMask;
+        fs->fold2[tid].out = c.ll + (sb % kLLFifoSlots) * (uint64_t)c.llSlotLines;
+        fs->fold2[tid].sflag = (uint32_t)(sb + 1) & llFlagMask;
+        const DevRecvConn& r = fs->foldRecv[tid];
+        const uint64_t ra = r.step + 2 * i - 2, rb = r.step + 2 * i - 3;  // A(i - 1), B(i - 2)
+        fs->fold[tid].in = r.ll + (ra % kLLFifoSlots) * (uint64_t)slotLines;
+        fs->fold[tid].rflag = (uint32_t)(ra + 1) & llFlagMask;
+        fs->fold2[tid].in = r.ll + (rb % kLLFifoSlots) * (uint64_t)slotLines;
+        fs->fold2[tid].rflag = (uint32_t)(rb + 1) & llFlagMask;
+      }
+      __syncthreads();
+      if (doA) {
+        // A(i): this rank's packs of every peer's set, 8 peers' loads in flight
+        const int ns = nsOf(i);
+        for (int q = tid; q < ns; q += kNT) {
+          int j, pos;
+          packOf(i, q, j, pos);
+          const uint32_t o0 = (uint32_t)llLineIdx(q, 0) * 16, o1 = (uint32_t)llLineIdx(q, 1) * 16;
+          for (int g0 = 0; g0 < np; g0 += G) {
+            u32x4 v[G];
+#pragma unroll
+            for (int k = 0; k < G; k++)
+              if (g0 + k < np) v[k] = loadPack(srs, vec, (int)lists[(g0 + k) * K + j] * Q + pos, n);
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              if (g0 + k >= np) continue;
+              const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold[g0 + k].out);
+              const uint32_t f = fs->fold[g0 + k].sflag;
+              st16<kAuxFifo>(frs, o0, (u32x4){v[k].x, f, v[k].y, f});
+              st16<kAuxFifo>(frs, o1, (u32x4){v[k].z, f, v[k].w, f});
+            }
+          }
+        }
+      }
+      if (doB) {
+        // B(i - 1): fold the own set from every peer's A lines, store, send the result
+        const int ns = nsOf(i - 1);
+        for (int q = tid; q < ns; q += kNT) {
+          int j, pos;
+          packOf(i - 1, q, j, pos);
+          const uint32_t o0 = (uint32_t)llLineIdx(q, 0) * 16, o1 = (uint32_t)llLineIdx(q, 1) * 16;
+          const int c = lists[np * K + j];
+          const int B = c * Q + pos;
+          const u32x4 own = loadPack(srs, vec, B, n);
+          const int cls = fs->chunkClass[c];
+          const uint8_t* pm = fs->cperm[cls];
+          const int ownPos = fs->cown[cls];
+          u32x4 acc = (u32x4){0, 0, 0, 0};
+          bool first = true;
+          for (int g0 = 0; g0 < np; g0 += G) {
+            const void* la[2 * G];
+            int pk[G];
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              pk[k] = pm[g0 + k < np ? g0 + k : g0];
+              const char* in = (const char*)fs->fold[pk[k]].in;
+              la[2 * k] = in + o0;
+              la[2 * k + 1] = in + o1;
+            }
+            u32x4 ln[2 * G];
+            ldLines16(la, ln);
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              const int p = g0 + k;
+              if (p >= np) continue;
+              if (p == ownPos) {
+                acc = first ? own : F::pack(acc, own);
+                first = false;
+              }
+              const uint32_t rflag = fs->fold[pk[k]].rflag;
+              Spin spins;
+              while (ln[2 * k].y != rflag || ln[2 * k].w != rflag || ln[2 * k + 1].y != rflag ||
+                     ln[2 * k + 1].w != rflag) {
+                if (spinAbort(spins)) break;
+                ldLines2(la[2 * k], la[2 * k + 1], ln[2 * k], ln[2 * k + 1]);
+              }
+              const u32x4 peer = {ln[2 * k].x, ln[2 * k].z, ln[2 * k + 1].x, ln[2 * k + 1].z};
+              acc = first ? peer : F::pack(acc, peer);
+              first = false;
+            }
+          }
+          if (ownPos == np) acc = first ? own : F::pack(acc, own);
+          storePack(drs, vec, B, n, acc);
+          for (int k = 0; k < np; k++) {
+            const __amdgpu_buffer_rsrc_t frs = makeRsrc(fs->fold2[k].out);
+            const uint32_t f = fs->fold2[k].sflag;
+            st16<kAuxFifo>(frs, o0, (u32x4){acc.x, f, acc.y, f});
+            st16<kAuxFifo>(frs, o1, (u32x4){acc.z, f, acc.w, f});
+          }
+        }
+      }
+      if (doC) {
+        // C(i - 2): every owner's result to its place, 8 peers per wait
+        const int ns = nsOf(i - 2);
+        for (int q = tid; q < ns; q += kNT) {
+          int j, pos;
+          packOf(i - 2, q, j, pos);
+          const uint32_t o0 = (uint32_t)llLineIdx(q, 0) * 16, o1 = (uint32_t)llLineIdx(q, 1) * 16;
+          for (int g0 = 0; g0 < np; g0 += G) {
+            const void* la[2 * G];
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              const char* in = (const char*)fs->fold2[g0 + k < np ? g0 + k : g0].in;
+              la[2 * k] = in + o0;
+              la[2 * k + 1] = in + o1;
+            }
+            u32x4 ln[2 * G];
+            ldLines16(la, ln);
+#pragma unroll
+            for (int k = 0; k < G; k++) {
+              if (g0 + k >= np) continue;
+              const uint32_t rflag = fs->fold2[g0 + k].rflag;
+              Spin spins;
+              while (ln[2 * k].y != rflag || ln[2 * k].w != rflag || ln[2 * k + 1].y != rflag ||
+                     ln[2 * k + 1].w != rflag) {
+                if (spinAbort(spins)) break;
+                ldLines2(la[2 * k], la[2 * k + 1], ln[2 * k], ln[2 * k + 1]);
+              }
+              storePack(drs, vec, (int)lists[(g0 + k) * K + j] * Q + pos, n,
+                        (u32x4){ln[2 * k].x, ln[2 * k].z, ln[2 * k + 1].x, ln[2 * k + 1].z});
+            }
+          }
+        }
+      }
+      for (int k = 0; k < np; k++) {
+        // LL cleanup (prims_ll.h:90-97): on cleanup steps stamp the unused lines of a slot sent
+        const uint64_t b = uni(fs->foldSend[k].step);
+        for (int h2 = 0; h2 < 2; h2++) {
+          if (h2 == 0 ? !doA : !doB) continue;
+          const uint64_t st = h2 == 0 ? b + 2 * i : b + 2 * i - 1;
+          if ((st & llCleanMask) != llCleanMask) continue;
+          const int ns = nsOf(h2 == 0 ? i : i - 1);
+          const FoldShared::Peer& pr = h2 == 0 ? fs->fold[k] : fs->fold2[k];
+          const __amdgpu_buffer_rsrc_t frs = makeRsrc(pr.out);
+          const uint32_t f = pr.sflag;
+          for (int l = tid; l < slotLines; l += kNT) {
+            const int q = ((l >> 7) << 6) + (l & 63);
+            if (q >= ns) st16<kAuxFifo>(frs, (uint32_t)l * 16, (u32x4){0, f, 0, f});
+          }
+        }
+      }
+      __syncthreads();
+      if (tid < np && (doB || doC)) {
+        // consumed: A(0 .. a - 1), B(0 .. b - 1): free the prefix (head post)
+        const int a = min(i, nsteps), b = max(0, min(i - 1, nsteps));
+        const uint64_t head = fs->foldRecv[tid].step + (uint64_t)(a > b ? 2 * b + 1 : 2 * a);
+        atomicStoreSys(fs->foldRecv[tid].remoteHead, head);
+      }
+    }
+    if (tid < np) {  // both counters advance by the launch's slots
+      fs->foldSend[tid].step += 2 * (uint64_t)nsteps;
+      fs->foldRecv[tid].step += 2 * (uint64_t)nsteps;
+    }
+    __syncthreads();
+    if (tid < np) {  // persist the connections' steps (flat records of thread block k + 1)
+      DevSendConn* cg = sendG + (size_t)(tid + 1) * connSplit + wg;
+      cg->step = fs->foldSend[tid].step;
+      cg->headSeen = fs->foldSend[tid].headSeen;
+      (recvG + (size_t)(tid + 1) * connSplit + wg)->step = fs->foldRecv[tid].step;
+    }
+    // the epochs: slots [0, wgs) are this launch's workgroups', [wgs, epochSlots) advanced for the rest
+    if (tid == 0) atomicStoreAgent(epochs + wg, workIndex + 1);
+    for (int j = wgs + wg + tid * wgs; j < w.epochSlots; j += kNT * wgs) atomicStoreAgent(epochs + j, workIndex + 1);
+  }
+
   // ---------------------------------------------------------------- small calls
   // A launch whose every rank's call runs run()'s loop as equal passes: one iteration
   // (sizePerChunk <= chunkSize) or full iterations merged `merge` at a time with nothing left
@@ -1885,8 +2190,10 @@ struct PairRunner : Interp<T, OP, pLL> {
     Shape s;
     s.n = sizePer;
     s.Q = (int)Qc;
-    s.q0 = split == 1 ? 0 : (int)((Qc * (uint32_t)sub) >> lg);
-    s.Lq = split == 1 ? (int)Qc : (int)((Qc * (uint32_t)(sub + 1)) >> lg) - s.q0;
+    // (64-bit products: the lowered pair runs one chunk of up to 1 GiB over up to kMaxFlatSubs
+    // workgroups; where runSmall's 32-bit cut holds, both cut alike)
+    s.q0 = split == 1 ? 0 : (int)(((uint64_t)Qc * (uint32_t)sub) >> lg);
+    s.Lq = split == 1 ? (int)Qc : (int)(((uint64_t)Qc * (uint32_t)(sub + 1)) >> lg) - s.q0;
     s.npk = s.Lq;
     // one round trip: this lane's packs q = tid + u * kNT of step 0 (llFusedOp uses those with
     // q < min(npk, slot packs) <= kNT * U), both connection records (wave 7), the epoch (wave 6)
@@ -2011,6 +2318,19 @@ __global__ void __launch_bounds__(kNT, 1) mscclFoldKernel(const LaunchArgsN<R> a
   Interp<T, OP, pLL> it;
   it.sh = &sh;
   it.runFold(w, b - w.blockBase, &fs);
+}
+
+// The two-phase fold (Interp::runTwoPhase): rank r of the launch owns workgroups [blockBase,
+// blockBase + nBlocks), one per flat sub-connection.
+template <typename T, int OP, int R>
+__global__ void __launch_bounds__(kNT, 1) mscclTwoPhaseKernel(const LaunchArgsN<R> args) {
+  __shared__ BlockShared sh;
+  __shared__ FoldShared fs;
+  const int b = blockIdx.x;
+  const RankWork& w = rankWorkOf(args, b);
+  Interp<T, OP, pLL> it;
+  it.sh = &sh;
+  it.runTwoPhase(w, b - w.blockBase, &fs);
 }
 
 }  // namespace msccl

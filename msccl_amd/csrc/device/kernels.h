@@ -69,6 +69,31 @@ int launchFoldKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// the two-phase fold (mscclTwoPhaseKernel, LL, Sum..Min): RankWork::nBlocks workgroups per rank
+template <typename T, int OP>
+int launchTwoPhaseKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  constexpr int RC = kCompactLaunchRanks;
+  if (gridBlocks == kQueryResidency) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclTwoPhaseKernel<T, OP, kMaxLaunchRanks>, kNT, 0) !=
+        hipSuccess)
+      return 0;
+    return n;
+  }
+  if (gridBlocks < args.nRanks) return 1;
+  if (args.nRanks <= RC) {
+    LaunchArgsN<RC> a;
+    a.nRanks = args.nRanks;
+    a.pad = 0;
+    for (int r = 0; r < RC; r++) a.w[r] = args.w[r];
+    hipLaunchKernelGGL((mscclTwoPhaseKernel<T, OP, RC>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL((mscclTwoPhaseKernel<T, OP, kMaxLaunchRanks>), dim3(gridBlocks), dim3(kNT), 0,
+                       (hipStream_t)stream, args);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // the pair kernel (mscclPairKernel, LL, Sum..Min): same contract as launchSmallKernel
 template <typename T, int OP>
 int launchPairKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
@@ -134,6 +159,8 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
                              launchFoldKernel<T, kMin>};                                                   \
   LaunchFn NAME##_pair[4] = {launchPairKernel<T, kSum>, launchPairKernel<T, kProd>, launchPairKernel<T, kMax>, \
                              launchPairKernel<T, kMin>};                                                   \
+  LaunchFn NAME##_two[4] = {launchTwoPhaseKernel<T, kSum>, launchTwoPhaseKernel<T, kProd>,                  \
+                            launchTwoPhaseKernel<T, kMax>, launchTwoPhaseKernel<T, kMin>};                 \
   extern const uint32_t NAME##_layout = kWorkLayout;
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \

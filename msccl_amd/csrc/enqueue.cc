@@ -166,10 +166,72 @@ RankWork makeFlatWork(Planned& p) {
   w.sizePerChunk = p.plan.sizePerChunk;
   w.chunkSize = p.plan.chunkSize;
   w.minChunk = p.plan.minChunk;
+  w.timeoutTicks = comm->timeoutTicks;
+  w.refNthreads = (int16_t)p.plan.refNthreads;
+  w.foldPeers = (uint8_t)(comm->nRanks - 1);
+  const int64_t pe = 16 / refTypeSize(p.plan.dtype);
+  if (p.plan.lowerMode == kLowerPair) {
+    // the pair kernel (interpreter.h: PairRunner) on peer record 0 of the flat connections: one
+    // chunk (the whole buffer), one thread block of W workgroups, one sub-connection each; W a
+    // power of two, at most flatSubs, at least kNT / 4 packs per workgroup (a function of the call
+    // and the agreed flatSubs only: both ranks cut the same FIFO steps)
+    const int64_t npk = (p.plan.count + pe - 1) / pe;
+    int wgs = 1;
+    while (wgs * 2 <= da.connSplit && npk >= (int64_t)wgs * 2 * (kNT / 4)) wgs *= 2;
+    w.send = da.dSend + da.connSplit;
+    w.recv = da.dRecv + da.connSplit;
+    w.maxSplit = da.connSplit;  // epoch slot of workgroup k: k
+    w.split = (uint8_t)wgs;
+    w.nBlocks = (int16_t)wgs;
+    w.merge = 1;
+    w.sizePerChunk = p.plan.count;
+    w.chunkSize = p.plan.count;  // one pass
+    w.pairSrc = 0;
+    w.pairDst = 0;
+    w.pairStride = 0;
+    w.pairDstBuf = (uint8_t)(p.inPlace ? 0 : 1);
+    w.maxAllowedCount = 1;
+    w.launchSeq = comm->workIndex++;
+    comm->last = {lowered, p.plan.proto, wgs, 1, kTreeFlat, 0, w.nBlocks};
+    return w;
+  }
+  if (p.plan.lowerMode == kLowerTwoPhase) {
+    // the two-phase fold (interpreter.h: runTwoPhase): W workgroups dealing every rank's owned
+    // packs M = K chunks x Q packs, at least kNT / 4 per workgroup (a function of the call and the
+    // agreed flatSubs only, so every rank deals alike)
+    const int64_t Q = p.plan.foldChunkPacks;
+    const int64_t M = Q * (p.plan.nchunksPerLoop / comm->nRanks);
+    int wgs = da.connSplit;
+    while (wgs > 1 && M < (int64_t)wgs * (kNT / 4)) wgs /= 2;
+    w.split = (uint8_t)wgs;
+    w.nBlocks = (int16_t)wgs;
+    w.merge = 1;
+    w.sizePerChunk = p.plan.count;  // the whole buffer (bound of every pack)
+    w.foldChunkPacks = (int32_t)Q;
+    w.foldPacksPerWg = (int32_t)(M / wgs);
+    w.tpOwnedPacks = (uint32_t)M;
+    // m / Q as ((t + ((m - t) >> sh1)) >> sh2), t = mulhi(m, magic) (Granlund and Montgomery,
+    // "Division by invariant integers using multiplication", fig. 4.1): exact for every 32-bit m
+    const uint32_t d = (uint32_t)Q;
+    const int l = d <= 1 ? 0 : 32 - __builtin_clz(d - 1);
+    w.tpMagic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+    w.tpSh1 = (uint8_t)std::min(l, 1);
+    w.tpSh2 = (uint8_t)std::max(l - 1, 0);
+    // packs per FIFO step (kTwoPhaseStepPacks, MSCCL_AMD_TWO_PHASE_STEP): agreed knobs, so both
+    // ends of every connection cut the same steps; at most a slot's
+    const int64_t slotPk = comm->llSlotLines / 2;
+    const int64_t stepPk = comm->knobs.twoPhaseStep > 0 ? comm->knobs.twoPhaseStep : kTwoPhaseStepPacks;
+    w.tpStepPacks = (uint16_t)std::max<int64_t>(64, std::min<int64_t>({stepPk, slotPk, 65535}));
+    w.ringColl = 0;
+    w.foldChunkPacks = (int32_t)Q;
+    w.maxAllowedCount = 1;
+    w.launchSeq = comm->workIndex++;
+    comm->last = {lowered, p.plan.proto, wgs, 1, kTreeFlat, 0, w.nBlocks};
+    return w;
+  }
   // workgroups per rank: one per kFoldPacksPerWg packs of the call, at most kFlatSubs (a function
   // of the call's size alone, so every rank picks the same and the two ends of every
   // sub-connection own the same packs; one workgroup against up to four: profiles/r03_ab_fold_wgs_and_r02.txt; 16 against 4: r04t_lat.txt)
-  const int64_t pe = 16 / refTypeSize(p.plan.dtype);
   const int64_t npk = (p.plan.sizePerChunk + pe - 1) / pe;
   const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>(kFlatSubs, (npk + kFoldPacksPerWg - 1) / kFoldPacksPerWg));
   w.split = (uint8_t)wgs;
@@ -236,10 +298,14 @@ RankWork makeWork(Planned& p) {
   if (comm->knobs.split <= 0)
     while (split > 1 && p.plan.sizePerChunk / pe < (int64_t)split * (kNT / 4)) split /= 2;
   // the wide budget (two co-resident LL ranks, plan.h: kWideSplitMinBytes) only while every
-  // workgroup still moves kWideSplitMinBytes of the call; nBytes is the same on every rank
+  // workgroup still moves kWideSplitMinBytes of the call.  Both inputs must be the same on every
+  // rank: nBytes is, and the thread-block count is the most over every rank's program
+  // (algoMaxBlocks, agreed at init) -- ranks of one schedule may run different numbers of thread
+  // blocks (topo.cc:1174-1184), and this rank's own count would let the two ends of a
+  // sub-connection step back differently
   if ((size_t)p.plan.algoIndex < comm->algoSplitBase.size())
     while (split > comm->algoSplitBase[p.plan.algoIndex] &&
-           p.plan.nBytes < (int64_t)da.nBlocks * split * kWideSplitMinBytes)
+           p.plan.nBytes < (int64_t)comm->algoMaxBlocks[p.plan.algoIndex] * split * kWideSplitMinBytes)
       split /= 2;
   w.split = (uint8_t)split;
   w.nBlocks = (int16_t)(da.nBlocks * split);
@@ -361,8 +427,12 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
     }
   }
   const Planned& p0 = *ps[0];
-  // a launch group holds flat-tree works only or none (executeOps keys launches on it)
-  const bool fold = p0.plan.ringColl == kTreeFlat;
+  // a launch group holds flat works of one lowering mode only, or none (executeOps keys launches
+  // on it): the fold, the pair kernel on the flat connections, or the two-phase fold
+  const bool flatWork = p0.plan.ringColl == kTreeFlat;
+  const bool fold = flatWork && p0.plan.lowerMode == kLowerFold;
+  const bool lowPair = flatWork && p0.plan.lowerMode == kLowerPair;
+  const bool two = flatWork && p0.plan.lowerMode == kLowerTwoPhase;
   // the small kernel holding only the exchange's transfers when every work of the launch needs
   // no more (devcomm.h: kSetExchange)
   int set = kSetExchange;
@@ -373,19 +443,26 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   }
   // the pair kernel (interpreter.h: PairRunner) when every work is a pair-form schedule whose call
   // is one pass of runSmall's loop, untraced
-  bool pair = small && !fold && set == kSetExchange && p0.op.comm->knobs.pairKernel;
+  bool pair = small && !flatWork && set == kSetExchange && p0.op.comm->knobs.pairKernel;
   for (int i = 0; i < args.nRanks && pair; i++) {
     const RankWork& w = args.w[i];
     pair = w.pairSrc >= 0 && w.trace == nullptr && w.sizePerChunk <= w.chunkSize * std::max<int>(1, w.merge);
   }
+  // (the lowered pair runs the pair kernel whatever MSCCL_AMD_PAIR_KERNEL says: both ends of its
+  // flat connections run it, the plan being the same on every rank)
+  pair = pair || lowPair;
   LaunchFn fn = fold ? getFoldLaunchFn(p0.plan.dtype, p0.op.devOp)
-                     : pair ? getPairLaunchFn(p0.plan.dtype, p0.op.devOp)
-                     : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp, set)
-                             : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
+                : two ? getTwoPhaseLaunchFn(p0.plan.dtype, p0.op.devOp)
+                : pair ? getPairLaunchFn(p0.plan.dtype, p0.op.devOp)
+                : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp, set)
+                        : getLaunchFn(p0.plan.dtype, p0.op.devOp, p0.plan.proto);
   for (Planned* p : ps) {
-    p->op.comm->last.small = fold ? 2 : small ? 1 : 0;
-    p->op.comm->last.set = small ? set : 0;
+    // small: 0 the general kernel, 1 the small-call kernel, 2 a flat kernel (fold, lowered pair,
+    // two-phase); kernel: 0 general, 1 small, 2 fold, 3 pair, 4 two-phase
+    p->op.comm->last.small = flatWork ? 2 : small ? 1 : 0;
+    p->op.comm->last.set = small && !flatWork ? set : 0;
     p->op.comm->last.pair = pair ? 1 : 0;
+    p->op.comm->last.kernel = fold ? 2 : two ? 4 : pair ? 3 : small ? 1 : 0;
   }
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {
@@ -465,7 +542,7 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
     }
     if (res != ncclSuccess) break;
     // copies / one-rank scaling run at once; kernels are fused per (device, type, op, protocol)
-    typedef std::tuple<int, int, int, int, bool> LaunchKey;  // + flat tree (its own kernel)
+    typedef std::tuple<int, int, int, int, int> LaunchKey;  // + flat kind: 0 none, 1 + lowerMode (own kernels)
     std::vector<std::pair<LaunchKey, std::vector<Planned*>>> launches;
     for (auto& p : planned) {
       if (p.noop) continue;
@@ -486,7 +563,8 @@ ncclResult_t executeOps(std::vector<CollOp>& ops) {
         continue;
       }
       const LaunchKey key =
-          std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto, p.plan.ringColl == kTreeFlat);
+          std::make_tuple(p.op.comm->cudaDev, p.plan.dtype, p.op.devOp, p.plan.proto,
+                          p.plan.ringColl == kTreeFlat ? 1 + p.plan.lowerMode : 0);
       size_t j = 0;
       while (j < launches.size() && launches[j].first != key) j++;
       if (j == launches.size()) launches.emplace_back(key, std::vector<Planned*>());

@@ -56,10 +56,12 @@ void analyzeLowering(ncclComm* comm) {
       ncclComm::FoldProgram& f = comm->algoFold[g];
       f.chunkClass = fl.chunkClass;
       for (auto& perRank : fl.order) f.order.push_back(perRank[comm->rank]);
+      if (fl.twoPhase) f.owner = fl.owner;
     }
-    INFO(kSubInit, "MSCCL: algorithm %s %s", a.name.c_str(),
+    INFO(kSubInit, "MSCCL: algorithm %s %s%s", a.name.c_str(),
          fl.ok ? "is a one-hop fold: calls up to MSCCL_AMD_LOWER_MAX_BYTES run the fold kernel"
-               : ("runs interpreted (" + fl.why + ")").c_str());
+               : ("runs interpreted (" + fl.why + ")").c_str(),
+         !fl.ok ? "" : fl.twoPhase ? "; larger calls run its two-phase form" : (", not two-phase: " + fl.whyNotTwoPhase).c_str());
   }
 }
 
@@ -123,7 +125,8 @@ struct SplitRecord {
   int32_t sendRun[kMaxAlgos];
   int32_t nFuse[kMaxAlgos];
   int16_t fuse[kMaxAlgos][kMaxFuse][2];  // (channel, peer) of each fusable exchange (fusableTbs)
-  uint8_t lowered[kMaxAlgos];             // analyzeLowering found the schedule a one-hop fold
+  uint8_t lowered[kMaxAlgos];             // analyzeLowering found the schedule a one-hop fold (1), with a
+                                          // two-phase form (3)
   uint8_t pairShape[kMaxAlgos];           // in pair form when its offered exchanges fuse (pairFormOf)
   uint8_t pairRun[kMaxAlgos];             // pairShape and the pair kernel on
   Knobs knobs;
@@ -139,7 +142,9 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
   for (size_t a = 0; a < comm->algos.size() && a < (size_t)kMaxAlgos; a++) {
     s.nBlocks[a] = comm->algos[a].nBlocks;
     s.sendRun[a] = algoSendRunOf(comm->algos[a]);
-    s.lowered[a] = a < comm->algoFold.size() && !comm->algoFold[a].order.empty();
+    s.lowered[a] = a < comm->algoFold.size() && !comm->algoFold[a].order.empty()
+                       ? (comm->algoFold[a].owner.empty() ? 1 : 3)
+                       : 0;
     const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
     s.pairShape[a] = comm->knobs.fuse && pairFormOf(comm->algos[a], fc).src >= 0;
     s.pairRun[a] = s.pairShape[a] && comm->knobs.pairKernel;
@@ -181,6 +186,9 @@ static std::string knobDiff(const Knobs& a, const Knobs& b) {
   add(a.treeFlat != b.treeFlat, "MSCCL_AMD_TREE_FLAT");
   add(a.lower != b.lower, "MSCCL_AMD_LOWER");
   add(a.lowerMaxBytes != b.lowerMaxBytes, "MSCCL_AMD_LOWER_MAX_BYTES");
+  add(a.lowerLarge != b.lowerLarge, "MSCCL_AMD_LOWER_LARGE");
+  add(a.forceRemote != b.forceRemote, "MSCCL_AMD_FORCE_REMOTE");
+  add(a.twoPhaseStep != b.twoPhaseStep, "MSCCL_AMD_TWO_PHASE_STEP");
   return out.empty() ? "(unnamed field)" : out;
 }
 
@@ -211,6 +219,7 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
   for (auto& q : recs) comm->coResident += !strcmp(mine.host, q.host) && !strcmp(mine.bus, q.bus);
   comm->algoSplit.assign(comm->algos.size(), 1);
   comm->algoSplitBase.assign(comm->algos.size(), 1);
+  comm->algoMaxBlocks.assign(comm->algos.size(), 1);
   comm->algoSendRun.assign(comm->algos.size(), 1);
   comm->maxSplit = 1;
   for (size_t a = 0; a < comm->algos.size(); a++) {
@@ -224,6 +233,7 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     const bool wide = maxCo == 2 && comm->algos[a].proto == kProtoLL;
     comm->algoSplit[a] = chooseSplit(mb, maxCo, comm->knobs, comm->algos[a].proto, wide);
     comm->algoSplitBase[a] = chooseSplit(mb, maxCo, comm->knobs, comm->algos[a].proto);
+    comm->algoMaxBlocks[a] = std::max(1, mb);
     comm->algoSendRun[a] = run;
     comm->maxSplit = std::max(comm->maxSplit, comm->algoSplit[a]);
   }
@@ -245,6 +255,26 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
       pairEverywhere = pairEverywhere && (int)a < r.nAlgos && r.pairRun[a];
     }
     if (pairEverywhere) comm->algoFold[a] = ncclComm::FoldProgram();
+    // the two-phase form only where every rank found it (each rank analysed every rank's program)
+    for (auto& r : recs)
+      if ((int)a >= r.nAlgos || (r.lowered[a] & 2) == 0) comm->algoFold[a].owner.clear();
+  }
+  // Lowered large calls (plan.cc: lowerLargePlan): 2 ranks run the pair kernel on the flat
+  // connections, more ranks the two-phase fold, each with up to flatSubs workgroups per rank and
+  // one flat sub-connection per workgroup: one workgroup per CU over the GPU's co-resident ranks
+  // (MSCCL_AMD_TARGET_WGS, default 256), at least kFlatSubs (the fold kernel's).  Agreed: the
+  // same records on every rank.
+  comm->flatSubs = kFlatSubs;
+  if (comm->knobs.lowerLarge) {
+    bool any = false;
+    for (size_t a = 0; a < comm->algoFold.size(); a++)
+      any = any || (!comm->algoFold[a].order.empty() && (recs.size() == 2 || !comm->algoFold[a].owner.empty()));
+    if (any) {
+      const int target = comm->knobs.targetWgs > 0 ? comm->knobs.targetWgs : 256;
+      int w = kFlatSubs;
+      while (w * 2 <= kMaxFlatSubs && (int64_t)w * 2 * maxCo <= target) w *= 2;
+      comm->flatSubs = w;
+    }
   }
   // a schedule in pair form on every rank merges its calls into one pass (enqueue.cc: makeWork);
   // the pass cut decides which workgroup owns which positions, so every rank must agree on it
@@ -287,8 +317,8 @@ static ncclResult_t allocSlots(ncclComm* comm) {
   };
   for (DevAlgoHost& d : comm->devAlgos) take(d, std::max(1, d.nBlocks) * comm->maxSplit);
   for (int k = 0; k < 5; k++) take(comm->ringAlgos[k], std::max(1, comm->ringAlgos[k].nBlocks) * comm->maxSplit);
-  take(comm->ringAlgos[5], kFlatSubs);
-  for (DevAlgoHost& d : comm->foldAlgos) take(d, kFlatSubs);  // lowered schedules (lower.cc)
+  take(comm->ringAlgos[5], comm->flatSubs);
+  for (DevAlgoHost& d : comm->foldAlgos) take(d, comm->flatSubs);  // lowered schedules (lower.cc)
   comm->slotTotal = total;
   const size_t flagWords = (size_t)total * kFlagStride + total;
   NCCLCHECK(hipErr(hipMalloc(&comm->dFlags, flagWords * sizeof(uint64_t)), "hipMalloc flags"));
@@ -302,13 +332,17 @@ static ncclResult_t allocSlots(ncclComm* comm) {
 
 ncclResult_t commFinish(ncclComm* comm) {
   comm->foldClasses.assign(comm->algos.size(), 0);
-  for (size_t a = 0; a < comm->algoFold.size() && a < comm->algos.size(); a++)
+  comm->foldTwoPhase.assign(comm->algos.size(), 0);
+  for (size_t a = 0; a < comm->algoFold.size() && a < comm->algos.size(); a++) {
     comm->foldClasses[a] = (int)comm->algoFold[a].order.size();
+    comm->foldTwoPhase[a] = comm->algoFold[a].owner.empty() ? 0 : 1;
+  }
   PlanContext& pc = comm->planCtx;
   pc.algos = &comm->algos;
   pc.regs = &comm->regs;
   pc.knobs = &comm->knobs;
   pc.foldClasses = &comm->foldClasses;
+  pc.foldTwoPhase = &comm->foldTwoPhase;
   pc.flat = flatEnabled(comm);
   pc.ringFallback = comm->ringFallback;
   pc.scratchSize = comm->scratchSize;
@@ -382,8 +416,10 @@ ncclResult_t initRankSync(ncclComm* comm, const ncclUniqueId& id) {
     // a peer is remote (xGMI) unless it runs on the same GPU: same host and PCI bus id
     std::vector<int> peerRemote(n, 0);
     for (int r = 0; r < n; r++) {
+      // MSCCL_AMD_FORCE_REMOTE: a test knob (xGMI ordering on one GPU), agreed through the knobs
+      // (it changes the lowering limit, plan.cc: defaultLowerMaxBytes)
       peerRemote[r] = strcmp(recs[r].host, srec.host) != 0 || strcmp(recs[r].bus, srec.bus) != 0 ||
-                      envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;  // test knob: xGMI ordering on one GPU
+                      comm->knobs.forceRemote != 0;
       if (r != comm->rank && peerRemote[r]) comm->anyRemote = true;
     }
     for (int r = 0; r < n; r++) {
@@ -569,7 +605,7 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
       }
       std::vector<int> remote(ndev);
       for (int j = 0; j < ndev; j++) {
-        remote[j] = cs[j]->cudaDev != cs[i]->cudaDev || envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;
+        remote[j] = cs[j]->cudaDev != cs[i]->cudaDev || cs[i]->knobs.forceRemote != 0;
         if (j != i && remote[j]) cs[i]->anyRemote = true;
       }
       cs[i]->peerArena = bases;

@@ -59,21 +59,26 @@ class Exprs {
     auto it = leaves_.find(key);
     if (it != leaves_.end()) return it->second;
     nodes_.push_back({-1, key});
+    creator_.push_back(rank);
     return leaves_[key] = (int)nodes_.size() - 1;
   }
-  int op(int x, int y) {
+  // fn(x, y) computed by a transfer of `rank` (the first rank to compute a value creates it)
+  int op(int x, int y, int rank) {
     if (x < 0 || y < 0) return kUndef;  // an uninitialised chunk poisons the result
     const std::pair<int, int> k = x < y ? std::make_pair(x, y) : std::make_pair(y, x);
     auto it = ops_.find(k);
     if (it != ops_.end()) return it->second;
     nodes_.push_back({k.first, k.second});
+    creator_.push_back(rank);
     return ops_[k] = (int)nodes_.size() - 1;
   }
   const Expr& at(int i) const { return nodes_[i]; }
+  int creator(int i) const { return creator_[i]; }
   static constexpr int kUndef = -1;
 
  private:
   std::vector<Expr> nodes_;
+  std::vector<int> creator_;
   std::map<int, int> leaves_;
   std::map<std::pair<int, int>, int> ops_;
 };
@@ -191,7 +196,7 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
             case kRecvReduceCopy:
             case kRecvReduceCopySend:
               for (int c = 0; c < cnt; c++) {
-                const int v = ex.op(msg[c], rd(src, t.srcoff + c));  // fn(peer, local)
+                const int v = ex.op(msg[c], rd(src, t.srcoff + c), r);  // fn(peer, local)
                 if (t.type != kRecvReduceSend && !wr(dst, t.dstoff + c, v)) return fail("write to a missing chunk");
                 if (t.type != kRecvReduceCopy) outMsg.push_back(v);
               }
@@ -206,7 +211,7 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
             case kReduce:
               for (int c = 0; c < cnt; c++) {
                 int acc = rd(dst, t.dstoff + c);
-                for (int j = 0; j < t.numReds; j++) acc = ex.op(acc, rd(src, tb.redSrcOff[t.redPtr + j] + c));
+                for (int j = 0; j < t.numReds; j++) acc = ex.op(acc, rd(src, tb.redSrcOff[t.redPtr + j] + c), r);
                 if (!wr(dst, t.dstoff + c, acc)) return fail("reduce into a missing chunk");
               }
               break;
@@ -282,6 +287,31 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
   if ((int)out.order.size() > kMaxFoldClasses) return fail("more fold orders than the fold kernel holds");
   if (out.order.size() > 1 && C > kMaxFoldChunks) return fail("more chunks than the fold kernel's class map holds");
   out.ok = true;
+  // the two-phase form: every rank's chunk c is the same value (hash-consed: the same node), and
+  // its creator owns it; every rank must own C / n chunks (the kernel deals the owned chunks of all
+  // ranks out to its workgroups in lockstep)
+  auto notTwoPhase = [&](const std::string& why) {
+    out.twoPhase = false;
+    out.whyNotTwoPhase = why;
+    out.owner.clear();
+    return out;
+  };
+  if (C > kMaxFoldChunks) return notTwoPhase("more chunks than the two-phase kernel's tables hold");
+  if (C % n != 0) return notTwoPhase("the chunks do not divide over the ranks");
+  out.owner.assign(C, -1);
+  std::vector<int> owned(n, 0);
+  for (int c = 0; c < C; c++) {
+    const int e = byRank[0].inPlace ? inB[0][c] : outB[0][c];
+    for (int r = 1; r < n; r++)
+      if ((byRank[r].inPlace ? inB[r][c] : outB[r][c]) != e)
+        return notTwoPhase("ranks hold different folds of a chunk (a one-shot schedule)");
+    const int q = ex.creator(e);
+    out.owner[c] = q;
+    owned[q]++;
+  }
+  for (int q = 0; q < n; q++)
+    if (owned[q] != C / n) return notTwoPhase("ranks own different numbers of chunks");
+  out.twoPhase = true;
   return out;
 }
 

@@ -15,11 +15,22 @@ namespace msccl {
 // two-phase all-pairs: one per chunk owner, who folds its own chunk first):
 //   chunkClass[c]       the class of chunk c (classes numbered by their first chunk);
 //   order[k][r]         the fold order (ranks) of class k on rank r.
+//
+// twoPhase: besides, every rank's result chunk c is one and the same expression (every rank holds
+// the bits its owner computed), and every rank owns C / n chunks; owner[c] is the rank whose
+// transfer computed chunk c's final fold (the msccl-tools two-phase all-pairs: the rank whose
+// `re` folds it, before its `s` hands it to the peers).  The two-phase fold kernel then runs the
+// schedule's dataflow without its scratch round trip: every rank sends chunk c of its input to
+// owner[c]; the owner folds the n copies straight from the FIFO lines in order[class(c)][owner]
+// and sends the result to every peer (interpreter.h: runTwoPhase).
 struct FoldLowering {
   bool ok = false;
   std::string why;
   std::vector<int> chunkClass;
   std::vector<std::vector<std::vector<int>>> order;
+  bool twoPhase = false;
+  std::string whyNotTwoPhase;
+  std::vector<int> owner;
 };
 FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank);
 // The schedule file at `path` loaded for each of nRanks ranks, then analyzeFoldLowering; cached

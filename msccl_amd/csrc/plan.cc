@@ -85,6 +85,9 @@ Knobs Knobs::fromEnv() {
   k.treeFlat = envInt("MSCCL_AMD_TREE_FLAT", 1) != 0;
   k.lower = envInt("MSCCL_AMD_LOWER", 1) != 0;
   k.lowerMaxBytes = envInt("MSCCL_AMD_LOWER_MAX_BYTES", -1);  // -1: by rank count (lowerToFoldPlan)
+  k.lowerLarge = envInt("MSCCL_AMD_LOWER_LARGE", 1) != 0;
+  k.forceRemote = envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;
+  k.twoPhaseStep = (int32_t)envInt("MSCCL_AMD_TWO_PHASE_STEP", 0);
   return k;
 }
 
@@ -319,13 +322,35 @@ int64_t defaultLowerMaxBytes(int nRanks, bool remote) {
   return p;
 }
 
-int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p) {
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, bool twoPhase, Plan* p) {
   const int64_t limit = k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : defaultLowerMaxBytes(c.nRanks, c.remote);
-  if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > limit ||
-      p->nBytes > (1ll << 30))
+  if (!k.lower || c.coll != kAllReduce || p->proto != kProtoLL || c.redop > kDevMin || p->nBytes > (1ll << 30))
     return 1;
   const int ts = refTypeSize(p->dtype);
   const int64_t pe = 16 / ts;
+  if (p->nBytes > limit) {
+    if (!k.lowerLarge) return 1;
+    int mode;
+    if (c.nRanks == 2) {
+      mode = kLowerPair;  // any fold of two inputs: fn(x_0, x_1) == fn(x_1, x_0) (lower.cc)
+    } else if (twoPhase && p->sizePerChunk % pe == 0 && p->nchunksPerLoop <= kMaxFoldChunks &&
+               p->sizePerChunk / pe * (p->nchunksPerLoop / c.nRanks) <= (int64_t)INT32_MAX) {
+      mode = kLowerTwoPhase;
+    } else {
+      return 1;
+    }
+    // one call over the whole buffer on the flat connections: no chunk loop, no FIFO merge rule,
+    // no scratch; the fields keep makePlan's meaning for introspection
+    p->lowerMode = mode;
+    p->foldChunkPacks = mode == kLowerTwoPhase ? p->sizePerChunk / pe : 0;
+    if (mode == kLowerPair) p->sizePerChunk = p->count;  // one chunk: the whole buffer
+    p->ringColl = kTreeFlat;
+    p->flatColl = kRingAllReduce;
+    p->ringChannels = 0;
+    p->maxAllowedCount = 1;
+    p->scratchNeeded = 0;
+    return 0;
+  }
   if (classes > 1 && (p->sizePerChunk % pe != 0 || p->nchunksPerLoop > kMaxFoldChunks)) return 1;
   p->foldChunkPacks = classes > 1 ? p->sizePerChunk / pe : 0;
   // the fold kernel's chunk math (makeFlatTreePlan): one call over the whole buffer
@@ -453,9 +478,12 @@ int planCall(const PlanContext& ctx, const CallDesc& c, bool asyncMany, Plan* p)
   const int r = makePlan(algos, idx, protoOverride, c, k, p);
   if (r != 0) return r;
   const int classes = ctx.foldClasses && (size_t)idx < ctx.foldClasses->size() ? (*ctx.foldClasses)[idx] : 0;
-  if (classes > 0 && ctx.flat && lowerToFoldPlan(c, k, classes, p) == 0) {
-    // a one-hop schedule (lower.cc): the fold kernel computes its values in one hop
-    INFO(kSubColl, "MSCCL: %s count=%zu runs as the one-hop fold", algos[idx].name.c_str(), c.count);
+  const bool twoPhase = ctx.foldTwoPhase && (size_t)idx < ctx.foldTwoPhase->size() && (*ctx.foldTwoPhase)[idx];
+  if (classes > 0 && ctx.flat && lowerToFoldPlan(c, k, classes, twoPhase, p) == 0) {
+    // a one-hop schedule (lower.cc): the fold kernel computes its values in one hop; larger calls
+    // the pair or the two-phase kernel
+    INFO(kSubColl, "MSCCL: %s count=%zu runs lowered (%s)", algos[idx].name.c_str(), c.count,
+         p->lowerMode == kLowerPair ? "pair exchange" : p->lowerMode == kLowerTwoPhase ? "two-phase fold" : "one-hop fold");
     return 0;
   }
   if (p->scratchNeeded > ctx.scratchSize) {

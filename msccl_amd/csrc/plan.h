@@ -52,7 +52,13 @@ struct Plan {
   int flatColl = 0;
   // a lowered schedule with several fold orders (lowerToFoldPlan): 16-B packs per chunk, else 0
   int64_t foldChunkPacks = 0;
+  // a lowered schedule's kernel (lowerToFoldPlan): kLowerFold, or for calls above the fold's
+  // limit kLowerPair (2 ranks) / kLowerTwoPhase
+  int lowerMode = 0;
 };
+enum : int { kLowerFold = 0, kLowerPair = 1, kLowerTwoPhase = 2 };
+// 16-B packs per FIFO step of the two-phase fold (a slot holds 2048 at the default LL FIFO)
+constexpr int64_t kTwoPhaseStepPacks = 1024;
 
 // Every environment knob the per-call planning reads, captured once at communicator init
 // (NCCL_PARAM caches its getenv the same way, include/param.h:99-108).  All ranks must plan
@@ -82,6 +88,10 @@ struct Knobs {
   int32_t simpleBuffEnv;     // NCCL_BUFFSIZE was set (else a communicator of one GPU takes kLocalSimpleBuff)
   int64_t lowerMaxBytes;     // MSCCL_AMD_LOWER_MAX_BYTES: largest call (bytes per rank) lowered (-1: by ranks)
   int32_t pairKernel;        // MSCCL_AMD_PAIR_KERNEL: pair-form exchanges take mscclPairKernel (rank-local)
+  int32_t lowerLarge;        // MSCCL_AMD_LOWER_LARGE: lowered calls above the fold's limit run lowered too
+                             // (2 ranks: the pair kernel; more: the two-phase fold; plan.cc: lowerLargePlan)
+  int32_t forceRemote;       // MSCCL_AMD_FORCE_REMOTE: every peer treated as on another GPU (a test knob)
+  int32_t twoPhaseStep;      // MSCCL_AMD_TWO_PHASE_STEP: 16-B packs per FIFO step of the two-phase fold (0: default)
   static Knobs fromEnv();
 };
 
@@ -142,7 +152,13 @@ int makeFlatTreePlan(const CallDesc& c, const Knobs& k, Plan* p);
 // schedule's own fold order, ncclComm::foldAlgos).  Returns 0, or nonzero (plan unchanged).
 // classes: the schedule's fold orders (lower.h); with several, the call's chunks must be whole
 // 16-B packs (each pack folds in its chunk's order).
-int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, Plan* p);
+// Calls above that limit (MSCCL_AMD_LOWER_LARGE, default on) run lowered as well, with the
+// schedule's values and without its scratch: 2 ranks as the pair exchange (each rank sends its
+// input, folds the peer's copy into its own: one hop, 6 S HBM bytes per rank against the two-phase
+// all-pairs' 7.5 S), more ranks as the two-phase fold when the schedule has that form
+// (twoPhase: lower.h) and its chunks are whole packs (9 S against the scratch form's 11.6 S at 8
+// ranks).  Otherwise nonzero: the interpreter runs the schedule.
+int lowerToFoldPlan(const CallDesc& c, const Knobs& k, int classes, bool twoPhase, Plan* p);
 // What a communicator's per-call planning reads besides the call itself (enqueue.cc: planOp).
 // The introspection mscclAmdLaunchPlanJson fills the same from XML files and a placement, so
 // what it reports is what a communicator of that placement launches.
@@ -151,6 +167,7 @@ struct PlanContext {
   const std::vector<Registration>* regs = nullptr;
   const Knobs* knobs = nullptr;                   // after init's agreed adjustments (FIFO sizes)
   const std::vector<int>* foldClasses = nullptr;  // per algorithm: fold orders when lowered, else 0
+  const std::vector<int>* foldTwoPhase = nullptr; // per algorithm: the lowering has a two-phase form
   bool flat = false;          // the flat group's connections exist (transport.cc: flatEnabled)
   bool ringFallback = true;   // MSCCL_AMD_RING_FALLBACK
   size_t scratchSize = 0;     // MSCCL scratch allocated at init

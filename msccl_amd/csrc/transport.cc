@@ -41,7 +41,7 @@ uint8_t groupProtoMask(const ncclComm* comm, int group) {
 }
 
 int groupSubs(const ncclComm* comm, int group) {
-  if (group == kFlatGroup) return kFlatSubs;  // one per fold workgroup (interpreter.h: runFold)
+  if (group == kFlatGroup) return comm->flatSubs;  // one per fold / pair / two-phase workgroup
   if (group == kRingGroup || group == kTreeGroup) return 1;  // the ring / tree fallbacks run unsplit
   return comm->algoSplit.empty() ? 1 : comm->algoSplit[group];
 }
@@ -471,8 +471,10 @@ ncclResult_t ringUpload(ncclComm* comm) {
     // schedule's are its own (lower.cc), one per class of chunks.  Tables in the image's reduction
     // list, one transfer each (positions map to peer records, -1 = this rank's input):
     //   0: the AllReduce fold order of class 0; 1: the ReduceScatter order; 2: the rank of every
-    //   peer record, then this rank; with several classes also 3: every class's order (srcoff =
-    //   classes) and 4: the class of every chunk (srcoff = chunks).
+    //   peer record, then this rank; with several classes (or a two-phase form) also 3: every
+    //   class's order (srcoff = classes) and 4: the class of every chunk (srcoff = chunks); with a
+    //   two-phase form (lower.h) also 5: the chunks each rank owns, ascending, per peer record and
+    //   then this rank's (srcoff = chunks per rank; interpreter.h: runTwoPhase).
     auto foldImage = [&](const ncclComm::FoldProgram& fp, DevAlgoHost& d) -> ncclResult_t {
     std::vector<int16_t> reds;
     const std::vector<int>& arOrder = fp.order[0];
@@ -483,8 +485,9 @@ ncclResult_t ringUpload(ncclComm* comm) {
     }
     for (int b = 1; b < n; b++) reds.push_back((int16_t)rp[b]);
     reds.push_back((int16_t)r);
-    const bool multi = fp.order.size() > 1;
-    std::vector<Transfer> ts(multi ? 5 : 3);
+    const bool two = !fp.owner.empty();
+    const bool multi = fp.order.size() > 1 || two;
+    std::vector<Transfer> ts(two ? 6 : multi ? 5 : 3);
     for (int i = 0; i < 3; i++) {
       ts[i].type = kFoldRecv;
       ts[i].srcbuf = kInput;
@@ -504,9 +507,25 @@ ncclResult_t ringUpload(ncclComm* comm) {
       ts[4].srcoff = (int16_t)fp.chunkClass.size();
       for (int k : fp.chunkClass) reds.push_back((int16_t)k);
     }
+    if (two) {
+      const int K = (int)fp.owner.size() / n;
+      ts[5] = ts[0];
+      ts[5].redPtr = (int16_t)reds.size();
+      ts[5].srcoff = (int16_t)K;
+      auto list = [&](int q) {
+        for (int c = 0; c < (int)fp.owner.size(); c++)
+          if (fp.owner[c] == q) reds.push_back((int16_t)c);
+      };
+      for (int b = 1; b < n; b++) list(rp[b]);
+      list(r);
+    }
+    if (imageBytes(ts.size(), 0, reds.size()) > (size_t)kMaxImage16 * 16) {  // the kernel's LDS copy (BlockShared::img)
+      WARN("MSCCL: the fold program of %d chunks does not fit a workgroup's image", (int)fp.chunkClass.size());
+      return ncclInternalError;
+    }
     d.nBlocks = 1;
     d.tbStride = (int)imageBytes(ts.size(), 0, reds.size());
-    d.connSplit = kFlatSubs;
+    d.connSplit = comm->flatSubs;
     d.dSend = comm->flatSend;
     d.dRecv = comm->flatRecv;
     std::vector<char> img((size_t)d.tbStride, 0);
@@ -620,7 +639,13 @@ ncclComm::PairForm pairFormOf(const Algorithm& a, const std::vector<FuseCandidat
     }
     pair = ts[0].srcoff == pf.src + b * pf.stride && ts[1].dstoff == pf.dst + b * pf.stride && ts[1].dstbuf == pf.dstBuf;
   }
-  return pair && pf.src < 32767 && pf.dst < 32767 ? pf : ncclComm::PairForm();
+  // RankWork carries src, dst and stride as int16: every one of them, and the last thread block's
+  // chunk indices, must fit (the indices are affine in b, so the first and last bound them all)
+  auto fits = [](int64_t x) { return x >= 0 && x < 32767; };
+  const int64_t last = (int64_t)std::max(0, a.nBlocks - 1) * pf.stride;
+  const bool ok = pair && fits(pf.src) && fits(pf.dst) && pf.stride >= -32767 && pf.stride < 32767 &&
+                  fits(pf.src + last) && fits(pf.dst + last);
+  return ok ? pf : ncclComm::PairForm();
 }
 
 // Pack every algorithm's per-tb programs into fixed-stride images and upload them (replaces

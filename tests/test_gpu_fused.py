@@ -20,6 +20,13 @@ pytestmark = pytest.mark.gpu
 os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
 
 
+@pytest.fixture(autouse=True)
+def _interpreter_kernels(monkeypatch):
+    """These tests pin the interpreter's fused exchange and the pair kernel on the schedules' own
+    connections: lowered large calls (tests/test_gpu_twophase.py) stay off."""
+    monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
+
+
 def _check(got, want, what):
     for r in range(len(want)):
         assert np.array_equal(np.asarray(got[r]).view(np.uint8), np.asarray(want[r]).view(np.uint8)), \

@@ -47,16 +47,21 @@ def _case(cr, count, dt, seed, op=0, in_place=True):
 @pytest.mark.parametrize("nbytes", [128, 1024, 4096, 16384, 32768])
 def test_c2_pair_tiers_lowered(tmp_path, nbytes, monkeypatch):
     """C2 (2 ranks, fp32) through bench.py's tiers: calls up to the limit run the fold kernel
-    (by default 4 KiB for 2 ranks; 32 KiB here), the rest the exchange-set small kernel."""
+    (by default 4 KiB for 2 ranks; 16 KiB here), the rest the pair kernel on the flat connections
+    (a lowered large call), or with MSCCL_AMD_LOWER_LARGE=0 the exchange-set small kernel."""
     monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", str(16 << 10))
     tiers = _bench().make_xmls(2, "LL", 16, str(tmp_path))
-    with CoResident(2, [open(t[3]).read() for t in tiers], str(tmp_path)) as cr:
-        for rep in range(3):
-            last, used = _case(cr, nbytes // 4, 7, 10 * rep + nbytes % 89)
-            if nbytes <= (16 << 10):
-                assert last["small"] == 2 and last["algo"] == used and last["ringColl"] == 5, last
-            else:
-                assert last["small"] == 1 and last["set"] == 1 and last["algo"] == used, last
+    for large in ("1", "0"):
+        monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", large)
+        with CoResident(2, [open(t[3]).read() for t in tiers], str(tmp_path)) as cr:
+            for rep in range(3):
+                last, used = _case(cr, nbytes // 4, 7, 10 * rep + nbytes % 89)
+                if nbytes <= (16 << 10):
+                    assert last["kernel"] == 2 and last["algo"] == used and last["ringColl"] == 5, last
+                elif large == "1":
+                    assert last["kernel"] == 3 and last["algo"] == used and last["ringColl"] == 5, last
+                else:
+                    assert last["small"] == 1 and last["set"] == 1 and last["algo"] == used, last
 
 
 @pytest.mark.parametrize("nbytes", [128, 2048, 8192])
@@ -86,7 +91,8 @@ def test_unordered_oneshot_every_op(tmp_path, op, monkeypatch):
 
 
 def test_knobs_and_limit(tmp_path, monkeypatch):
-    """MSCCL_AMD_LOWER=0 keeps the interpreter; calls above MSCCL_AMD_LOWER_MAX_BYTES keep it too."""
+    """MSCCL_AMD_LOWER=0 keeps the interpreter; calls above MSCCL_AMD_LOWER_MAX_BYTES run the
+    lowered pair (2 ranks), or with MSCCL_AMD_LOWER_LARGE=0 the interpreter too."""
     xml = xmlgen.allreduce_pair_oneshot(4, "LL")
     monkeypatch.setenv("MSCCL_AMD_LOWER", "0")
     with CoResident(2, [xml], str(tmp_path)) as cr:
@@ -95,8 +101,12 @@ def test_knobs_and_limit(tmp_path, monkeypatch):
     monkeypatch.setenv("MSCCL_AMD_LOWER", "1")
     monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "4096")
     with CoResident(2, [xml], str(tmp_path)) as cr:
-        assert _case(cr, 1024, 7, 2)[0]["small"] == 2
-        assert _case(cr, 1028, 7, 3)[0]["small"] == 1
+        assert _case(cr, 1024, 7, 2)[0]["kernel"] == 2
+        assert _case(cr, 1028, 7, 3)[0]["kernel"] == 3
+    monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        assert _case(cr, 1024, 7, 2)[0]["kernel"] == 2
+        assert _case(cr, 1028, 7, 3)[0]["kernel"] == 1
 
 
 def test_lowered_interpreted_and_flat_calls_interleave(tmp_path, monkeypatch):

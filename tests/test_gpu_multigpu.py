@@ -300,7 +300,7 @@ def _rank_proc8(rank, world, xml_path, jobs, q_in, q_out, one_gpu=False, env=Non
         torch.cuda.synchronize()
         outs.append(t.cpu().numpy())
         last = comm.info()["last"]
-        kernels.append(3 if last.get("pair") else last["small"])  # 0 general, 1 small, 2 fold, 3 pair kernel
+        kernels.append(last["kernel"])  # 0 general, 1 small, 2 fold, 3 pair, 4 two-phase kernel
     err = comm.async_error()
     remote = comm.info()["anyRemote"]
     comm.destroy()
@@ -369,13 +369,14 @@ def _check_c3_c5(res, c3, c5, jobs):
 @needs8
 def test_eight_processes_c3_c5_ipc(tmp_path):
     """One process per GPU (the reference's mpirun -np 8 -g 1, README.md:57): hipIpc FIFOs between
-    all 8 GPUs, C3's remote tiers (256 KiB lowered to the fold by the link model), then C5's
+    all 8 GPUs, C3's remote tiers (256 KiB lowered to the fold by the link model, 32 MiB to the
+    two-phase fold), then C5's
     ReduceScatter and AllGather, every rank bit-exact against the oracle."""
     c3, c5, jobs = _c3_c5_job(tmp_path, True)
     res = _eight_processes(tmp_path, c3 + c5, jobs)
     _check_c3_c5(res, c3, c5, jobs)
     assert all(res[r][3] == 1 for r in range(8))
-    assert [res[0][2][j] for j in range(4)] == [2, 2, 2, 1]  # fold up to 256 KiB, then the small kernel
+    assert [res[0][2][j] for j in range(4)] == [2, 2, 2, 4]  # fold up to 256 KiB, then the two-phase fold
 
 
 def test_eight_processes_one_gpu_c3_c5_ipc(tmp_path):
@@ -387,7 +388,7 @@ def test_eight_processes_one_gpu_c3_c5_ipc(tmp_path):
     res = _eight_processes(tmp_path, c3 + c5, jobs, one_gpu=True)
     _check_c3_c5(res, c3, c5, jobs)
     assert all(res[r][3] == 0 for r in range(8))
-    assert [res[0][2][j] for j in range(4)] == [2, 2, 1, 1]  # co-resident: fold up to 128 KiB
+    assert [res[0][2][j] for j in range(4)] == [2, 2, 4, 4]  # co-resident: fold up to 128 KiB, then two-phase
 
 
 def test_eight_processes_one_gpu_forced_remote(tmp_path):
@@ -400,7 +401,7 @@ def test_eight_processes_one_gpu_forced_remote(tmp_path):
     res = _eight_processes(tmp_path, c3 + c5, jobs, one_gpu=True, env={"MSCCL_AMD_FORCE_REMOTE": "1"})
     _check_c3_c5(res, c3, c5, jobs)
     assert all(res[r][3] == 1 for r in range(8))
-    assert [res[0][2][j] for j in range(4)] == [2, 2, 2, 1]  # the remote limit: the fold at 256 KiB
+    assert [res[0][2][j] for j in range(4)] == [2, 2, 2, 4]  # the remote limit: the fold at 256 KiB
 
 
 def _c4_job():
@@ -469,7 +470,7 @@ def test_four_processes_one_gpu_bench_tiers(tmp_path):
     xmls, jobs = _four_rank_job(tmp_path, False)
     res = _eight_processes(tmp_path, xmls, jobs, world=4, one_gpu=True)
     _check_four(res, xmls, jobs)
-    assert [res[0][2][j] for j in range(3)] == [2, 2, 1]
+    assert [res[0][2][j] for j in range(3)] == [2, 2, 4]
 
 
 # ------------------------------------------------------------------------------------------------

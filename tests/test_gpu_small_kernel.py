@@ -18,6 +18,13 @@ from oracle import numerics as N
 pytestmark = pytest.mark.gpu
 os.environ.setdefault("MSCCL_AMD_TIMEOUT_SEC", "20")
 
+
+@pytest.fixture(autouse=True)
+def _interpreter_kernels(monkeypatch):
+    """These tests pin the interpreter's kernels: lowered schedules' large calls (the pair kernel on
+    the flat connections, the two-phase fold: tests/test_gpu_twophase.py) stay off."""
+    monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
+
 SCHEDULES = {
     "pair2": (2, lambda: xmlgen.allreduce_pair_oneshot(1, "LL")),
     "allpairs8": (8, lambda: xmlgen.allreduce_allpairs(8, 1, "LL")),   # C3's form: reductions + deps
@@ -169,3 +176,42 @@ def test_two_rank_wide_split_by_call_size(tmp_path, count, split):
         want, _ = cr.oracle(L.ALLREDUCE, count, 7, 0, ins, True)
         for r in range(2):
             assert np.array_equal(got[r].view(np.uint32), want[r].view(np.uint32))
+
+
+def _uneven_pair_xml(inst: int) -> str:
+    """The 2-rank pair exchange (s, rrc per thread block) where rank 0 also runs `inst` thread
+    blocks of local copies (input chunk k to its scratch: value-neutral): the ranks run different
+    numbers of thread blocks (the reference computes nBlocks per gpu, topo.cc:1173-1185)."""
+    from msccl_amd.xmlgen import _Tb, _emit
+    gpus = {}
+    for r in range(2):
+        tbs = []
+        for k in range(inst):
+            tb = _Tb(k, 1 - r, 1 - r, k)
+            tb.add("s", "i", k, "i", k, 1)
+            tb.add("rrc", "i", k, "i", k, 1)
+            tbs.append(tb)
+        if r == 0:
+            for k in range(inst):
+                tb = _Tb(inst + k, -1, -1, k)
+                tb.add("cpy", "i", k, "s", k, 1)
+                tbs.append(tb)
+        gpus[r] = (inst, 0, inst if r == 0 else 0, tbs)
+    return _emit("uneven_pair", "LL", inst, inst, 2, "allreduce", True, gpus, 0, 1 << 40)
+
+
+@pytest.mark.parametrize("nbytes", [6 << 20, 3 << 20, 12 << 20])
+def test_wide_split_agrees_when_ranks_run_different_thread_block_counts(tmp_path, nbytes):
+    """the wide-split step-back compared against the rank's own thread-block
+    count.  Rank 0 runs 32 thread blocks, rank 1 16: at 6 MiB rank 0's count stepped its split back
+    to 4 while rank 1 kept 8, and the two ends of every sub-connection owned different packs (a hang
+    or wrong data).  Both now use the most over every rank's program (algoMaxBlocks); the oracle's
+    values at sizes inside and around the window."""
+    xml = _uneven_pair_xml(16)
+    with CoResident(2, [xml], str(tmp_path)) as cr:
+        ins, got, last = _run(cr, nbytes // 4, 7, 0, seed=nbytes % 89)
+        assert last[0]["split"] == last[1]["split"], last
+        want, _ = cr.oracle(L.ALLREDUCE, nbytes // 4, 7, 0, ins, True)
+        for r in range(2):
+            assert np.array_equal(got[r].view(np.uint32), want[r].view(np.uint32)), \
+                "rank %d: %s" % (r, describe_mismatch(got[r], want[r]))

@@ -47,8 +47,9 @@ def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
         assert v.get("scratch", 1) == 0, (k, v)
     for k, v in ks.items():
         # the flat tree's fold kernel runs one or a few workgroups per rank, never co-resident
-        # with each other on a CU by necessity: __launch_bounds__(512, 1) allows 256 VGPRs
-        limit = 256 if "mscclFoldKernel" in k else 128
+        # with each other on a CU by necessity, and the two-phase fold one workgroup per CU:
+        # __launch_bounds__(512, 1) allows 256 VGPRs
+        limit = 256 if "mscclFoldKernel" in k or "mscclTwoPhaseKernel" in k else 128
         assert v.get("vgpr", 999) <= limit, (k, v)
     fold = {k: v for k, v in ks.items() if re.search(r"mscclFoldKernelI(f|DF16_|NS_4Bf16E)Li[0-3]E", k)}
     assert len(fold) == 3 * 4 * 2, sorted(fold)
@@ -65,6 +66,11 @@ def test_hot_kernels_have_no_scratch_and_fit_two_workgroups_per_cu():
     pair = {k: v for k, v in ks.items() if re.search(r"mscclPairKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi(2|16)EE", k)}
     assert len(pair) == 3 * 4 * 2, sorted(pair)
     for k, v in pair.items():
+        assert v.get("scratch", 1) == 0, (k, v)
+    # the two-phase fold (interpreter.h: runTwoPhase), both argument blocks
+    two = {k: v for k, v in ks.items() if re.search(r"mscclTwoPhaseKernelI(f|DF16_|NS_4Bf16E)Li[0-3]ELi(2|16)EE", k)}
+    assert len(two) == 3 * 4 * 2, sorted(two)
+    for k, v in two.items():
         assert v.get("scratch", 1) == 0, (k, v)
 
 
@@ -136,7 +142,7 @@ def test_memory_asm_check_catches_an_sgpr_operand():
 
 def test_every_type_object_holds_every_kernel_family():
     """Each per-type kernel object (build/obj/device/kernels_<type>.res) was compiled from the
-    current kernels.h: it lists the general, small, fold and pair kernels (a stale object once
+    current kernels.h: it lists the general, small, fold, pair and two-phase kernels (a stale object once
     lacked the pair kernel and read RankWork at old offsets; init.cc also checks the layout stamp
     at run time)."""
     files = sorted(glob.glob(os.path.join(RES, "kernels_*.res")))
@@ -146,5 +152,5 @@ def test_every_type_object_holds_every_kernel_family():
     assert len(files) == 10, files
     for f in files:
         text = open(f).read()
-        for fam in ("mscclKernel", "mscclSmallKernel", "mscclFoldKernel", "mscclPairKernel"):
+        for fam in ("mscclKernel", "mscclSmallKernel", "mscclFoldKernel", "mscclPairKernel", "mscclTwoPhaseKernel"):
             assert re.search(r"Function Name: _ZN5msccl\d*%sI" % fam, text), (os.path.basename(f), fam)

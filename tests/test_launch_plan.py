@@ -47,24 +47,37 @@ def test_link_model_defaults():
 
 @pytest.mark.parametrize("nbytes,co,remote", [
     (128, "fold", "fold"), (64 << 10, "fold", "fold"), (128 << 10, "fold", "fold"),
-    (256 << 10, "interpreter", "fold"), (512 << 10, "interpreter", "interpreter"),
-    (32 << 20, "interpreter", "interpreter")])
+    (256 << 10, "twophase", "fold"), (512 << 10, "twophase", "twophase"),
+    (32 << 20, "twophase", "twophase")])
 def test_c3_tiers_by_placement(tmp_path, nbytes, co, remote):
     """bench.py's 8-rank tiers (C3, fp16): up to 128 KiB both placements run the fold; at 256 KiB
-    only ranks on different GPUs do (the link model), above neither."""
+    only ranks on different GPUs do (the link model); above, the two-phase all-pairs tiers run
+    their two-phase form (lower.h: FoldLowering::twoPhase), on either placement."""
     import bench
     tiers = bench.make_xmls(8, "LL", 8, str(tmp_path))
     files = ":".join(t[3] for t in tiers)
     for one_gpu, want in ((True, co), (False, remote)):
         got = M.launch_plan_json(files, 3, 8, one_gpu, L.ALLREDUCE, nbytes // 2, 6, 0, True)
         assert got["kernel"] == want, (one_gpu, got)
-        assert got["lowered"] == (want == "fold")
+        assert got["lowered"] == 1
         assert got["remote"] == (0 if one_gpu else 1)
+    import os
+    os.environ["MSCCL_AMD_LOWER_LARGE"] = "0"
+    try:
+        for one_gpu, want in ((True, co), (False, remote)):
+            got = M.launch_plan_json(files, 3, 8, one_gpu, L.ALLREDUCE, nbytes // 2, 6, 0, True)
+            assert got["kernel"] == (want if want == "fold" else "interpreter"), (one_gpu, got)
+    finally:
+        del os.environ["MSCCL_AMD_LOWER_LARGE"]
 
 
 def test_lower_limit_knob_overrides_both(tmp_path, monkeypatch):
     files = _files(tmp_path, [xmlgen.allreduce_allpairs(8, 1, "LL")])
     monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", "8192")
+    for one_gpu in (True, False):
+        got = M.launch_plan_json(files, 0, 8, one_gpu, L.ALLREDUCE, 16384 // 4, 7, 0, True)
+        assert got["lowerMaxBytes"] == 8192 and got["kernel"] == "twophase", got
+    monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
     for one_gpu in (True, False):
         got = M.launch_plan_json(files, 0, 8, one_gpu, L.ALLREDUCE, 16384 // 4, 7, 0, True)
         assert got["lowerMaxBytes"] == 8192 and got["kernel"] == "interpreter", got
@@ -144,11 +157,23 @@ def test_pair_kernel_knob_and_non_pair_schedules(tmp_path, monkeypatch):
     files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(16, "LL")])
     monkeypatch.setenv("MSCCL_AMD_PAIR_KERNEL", "0")
     got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 18, 7, 0, True)
+    # lowered instead (the pair kernel off the table leaves the schedule to the lowering): the
+    # lowered pair runs the pair kernel on the flat connections on both ends whatever the
+    # rank-local knob says
+    assert got["kernel"] == "pair" and got["lowered"] == 1 and got["pairForm"] == 1, got
+    monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 18, 7, 0, True)
     assert got["kernel"] == "interpreter" and got["pairForm"] == 1, got
+    monkeypatch.delenv("MSCCL_AMD_LOWER_LARGE")
     monkeypatch.delenv("MSCCL_AMD_PAIR_KERNEL")
     files = _files(tmp_path, [xmlgen.allreduce_allpairs(2, 16, "LL")])
     got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 20, 7, 0, True)
+    # the two-phase all-pairs of 2 ranks: its large calls run lowered as the pair exchange
+    assert got["kernel"] == "pair" and got["lowered"] == 1 and got["pairForm"] == 0, got
+    monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 20, 7, 0, True)
     assert got["kernel"] == "interpreter" and got["pairForm"] == 0, got
+    monkeypatch.delenv("MSCCL_AMD_LOWER_LARGE")
     # a call of more than 64 iterations stays on the interpreter (the one-pass merge caps at 64)
     files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(1, "LL")])
     got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 24, 7, 0, True)
