@@ -152,7 +152,7 @@ def schedule_bytes(algo: dict, size_per: int, ts: int, proto: int, payload_only:
 
 
 KERNEL_NAMES = {0: "mscclKernel", 1: "mscclSmallKernel", 2: "mscclFoldKernel (lowered)",
-                3: "mscclPairKernel", 4: "mscclTwoPhaseKernel (lowered)"}
+                3: "mscclPairKernel", 4: "mscclTwoPhaseKernel (lowered)", 5: "mscclDirectKernel (direct form)"}
 
 
 def kernel_name(last: dict) -> str:
@@ -423,7 +423,8 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 step()
                 torch.cuda.synchronize()
                 return agree(all(torch.equal(b.view(torch.uint8)[:S].view(tdt), want) for b in bufs))
-            phases = {"allreduce": (step, S * 2 * (n - 1) / n, launch_bytes(paths[0], cnt, 1, ts))}
+            # the direct form (kernel 5, lower.h: DirectLowering): every rank reads S and writes S
+            phases = {"allreduce": (step, S * 2 * (n - 1) / n, launch_bytes(paths[0], cnt, 1, ts), 2 * S * nloc)}
         else:
             rc = S // ts // n
             ins = [torch.empty(S // 4, dtype=torch.float32, device=dev).uniform_(-1, 1) for _ in range(nloc)]
@@ -450,11 +451,13 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 torch.cuda.synchronize()
                 good = all(torch.equal(m, full[r * rc:(r + 1) * rc]) for r, m in zip(ranks, mids))
                 return agree(good and all(torch.equal(o, full) for o in outs))
-            phases = {"reduce_scatter": (rs, S * (n - 1) / n, launch_bytes(paths[0], rc, n, ts)),
-                      "all_gather": (ag, S * (n - 1) / n, launch_bytes(paths[1], rc * ts, n, 1))}
+            # direct forms: the ReduceScatter reads every rank's block and writes its own ((n + 1) S / n
+            # per rank), the AllGather reads its block once and writes it n times (the same)
+            phases = {"reduce_scatter": (rs, S * (n - 1) / n, launch_bytes(paths[0], rc, n, ts), (n + 1) * (S // n) * nloc),
+                      "all_gather": (ag, S * (n - 1) / n, launch_bytes(paths[1], rc * ts, n, 1), (n + 1) * (S // n) * nloc)}
         res = {}
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for name, (fn, busbytes, algo_bytes) in phases.items():
+        for name, (fn, busbytes, algo_bytes, direct_bytes) in phases.items():
             note("%s warmup" % name)
             for _ in range(max(1, a.warmup)):
                 fn()
@@ -478,7 +481,10 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
                 t, ev_ms = float(tt[0]), float(tt[1])
             if any(c.async_error() != 0 for c in comms):
                 raise RuntimeError("kernel reported an error (timeout/abort)")
-            res[name] = {"ms": round(t * 1e3, 4), "kernel_ms": round(ev_ms, 4),
+            last = comms[0].info()["last"]
+            if last.get("kernel") == 5:
+                algo_bytes = direct_bytes
+            res[name] = {"ms": round(t * 1e3, 4), "kernel_ms": round(ev_ms, 4), "kernel": kernel_name(last),
                          "busbw": round(busbytes / t / 1e9, 3), "steps": k,
                          # roofline: algorithmic bytes of the launch on this GPU / its event time,
                          # against the 8 TB/s HBM peak.  Memory-side: FIFO slots and re-read blocks

@@ -29,8 +29,16 @@ int mscclAmdFusableJson(const char* xmlPath, int rank, int nranks, char* out, si
  * the one-hop fold (msccl_amd/csrc/lower.cc: every result chunk of every rank is a left fold of all
  * ranks' same chunk; chunks fall into classes of equal orders).  JSON {"ok":1,"classes":[[[ranks of
  * rank 0's fold], ... per rank], ... per class],"chunkClass":[class of chunk 0, ...]} or
- * {"ok":0,"why":"..."}.  No GPU needed. */
+ * {"ok":0,"why":"..."}.  With "ok":1 also "twoPhase":1 and every chunk's "owner" when every rank
+ * holds the same fold of every chunk and the ranks own equal shares (the two-phase fold of large
+ * calls), else "twoPhase":0 and "whyNotTwoPhase".  No GPU needed. */
 int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen);
+
+/* Whether a Simple AllReduce / ReduceScatter / AllGather schedule has the direct form (lower.h:
+ * DirectLowering; run when every rank of a communicator is in one launch).  JSON {"ok":1,"coll":c,
+ * "classes":[[[rank r's fold order], ... per rank], ... per class],"chunkClass":[...]} (the
+ * AllGather: no classes) or {"ok":0,"coll":c,"why":"..."}.  No GPU needed. */
+int mscclAmdDirectJson(const char* xmlPath, int nranks, char* out, size_t outLen);
 
 /* Select among the ':'-separated XML files (tuning.cc:344-382) and compute the schedule's chunk
  * plan (enqueue.cc:591-734), the reference's computeColl field by field, from the environment

@@ -88,6 +88,11 @@ def lib() -> ctypes.CDLL:
     L.mscclAmdFusableJson.argtypes = [ctypes.c_char_p, i, i, ctypes.c_char_p, sz]
     if hasattr(L, "mscclAmdLowerJson"):  # MSCCL_AMD_LIB may name an older build (A/B runs)
         L.mscclAmdLowerJson.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, sz]
+    if hasattr(L, "mscclAmdDirectJson"):
+        L.mscclAmdDirectJson.argtypes = [ctypes.c_char_p, i, ctypes.c_char_p, sz]
+    if hasattr(L, "mscclAmdKernelLayoutMismatch"):
+        L.mscclAmdKernelLayoutMismatch.argtypes = []
+        L.mscclAmdKernelLayoutMismatch.restype = ctypes.c_char_p
     L.mscclAmdPlanJson.argtypes = [ctypes.c_char_p, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
     if hasattr(L, "mscclAmdLaunchPlanJson"):  # MSCCL_AMD_LIB may name an older build (A/B runs)
         L.mscclAmdLaunchPlanJson.argtypes = [ctypes.c_char_p, i, i, i, i, sz, i, i, i, ctypes.c_char_p, sz]
@@ -157,6 +162,15 @@ def lower_json(xml_path: str, nranks: int) -> dict:
     each chunk]} or {"ok": 0, "why": reason}."""
     buf = ctypes.create_string_buffer(1 << 16)
     _check(lib().mscclAmdLowerJson(xml_path.encode(), nranks, buf, len(buf)), "mscclAmdLowerJson")
+    return json.loads(buf.value.decode())
+
+
+def direct_json(xml_path: str, nranks: int) -> dict:
+    """Whether a Simple AllReduce / ReduceScatter / AllGather schedule has the direct form (lower.h:
+    DirectLowering; it runs when every rank of a communicator is in one launch): {"ok": 1, "coll": c,
+    "classes": [[fold order of each rank] per class], "chunkClass": [...]} or {"ok": 0, "why": ...}."""
+    buf = ctypes.create_string_buffer(1 << 16)
+    _check(lib().mscclAmdDirectJson(xml_path.encode(), nranks, buf, len(buf)), "mscclAmdDirectJson")
     return json.loads(buf.value.decode())
 
 

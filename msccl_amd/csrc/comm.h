@@ -81,6 +81,18 @@ struct ncclComm {
     std::vector<int> owner;
   };
   std::vector<FoldProgram> algoFold;
+  // per algorithm: the direct form of a Simple schedule (lower.h: DirectLowering, agreed by every
+  // rank at init; coll -1: none) and its device program (directAlgos: the fold orders, RS / AR)
+  struct DirectProgram {
+    int coll = -1;
+    std::vector<int> chunkClass;
+    std::vector<std::vector<int>> order;  // this rank's fold order (ranks) per class
+  };
+  std::vector<DirectProgram> algoDirect;
+  std::vector<msccl::DevAlgoHost> directAlgos;
+  // communicators created together by one ncclCommInitAll with every rank on one device share a
+  // nonzero clique id: a group call of all of them is one fused launch (the direct form's condition)
+  uint64_t clique = 0;
   std::vector<int> algoSet;  // per algorithm: the small kernel's transfer set (transport.cc: algoUpload)
   // per algorithm: thread block b's program is one fused exchange of input chunk src + b * stride
   // into chunk dst + b * stride of buffer dstBuf (the pair kernel, RankWork::pairSrc); src -1: not
@@ -105,6 +117,7 @@ struct ncclComm {
   int coResident = 1;              // ranks of this communicator on this rank's GPU
   std::vector<int> foldClasses;    // per algorithm: algoFold's class count (0: not lowered)
   std::vector<int> foldTwoPhase;   // per algorithm: algoFold has the two-phase form (owner table)
+  std::vector<int> directClasses;  // per algorithm: the direct form's fold orders (AG: 1), 0: none
   msccl::PlanContext planCtx;      // what planCall reads (set at the end of init: commFinish)
 
   // transport
@@ -160,7 +173,8 @@ struct ncclComm {
     int algo = -2, proto = -1, split = 0, merge = 0, ringColl = 0, ringChannels = 0, blocks = 0, small = 0;
     int set = 0;  // the small kernel's transfer set (devcomm.h: kSetAll / kSetExchange)
     int pair = 0;  // the exchange ran in the pair kernel (mscclPairKernel)
-    int kernel = -1;  // 0 mscclKernel, 1 mscclSmallKernel, 2 mscclFoldKernel, 3 mscclPairKernel, 4 mscclTwoPhaseKernel
+    int kernel = -1;  // 0 mscclKernel, 1 mscclSmallKernel, 2 mscclFoldKernel, 3 mscclPairKernel, 4 mscclTwoPhaseKernel,
+                      // 5 mscclDirectKernel
   } last;
 
   // user reduction ops (ncclRedOpCreatePreMulSum, enqueue.cc:1529-1580): a free list as in the

@@ -94,6 +94,37 @@ int mscclAmdLowerJson(const char* xmlPath, int nranks, char* out, size_t outLen)
   return putOut(o.str(), out, outLen);
 }
 
+int mscclAmdDirectJson(const char* xmlPath, int nranks, char* out, size_t outLen) {
+  if (!xmlPath || nranks < 1) return ncclInvalidArgument;
+  std::vector<Algorithm> byRank(nranks);
+  for (int r = 0; r < nranks; r++) {
+    const int res = loadAlgoFromXml(xmlPath, &byRank[r], kMaxChannels, r, nranks);
+    if (res != 0) return res;
+  }
+  const DirectLowering dl = analyzeDirectLowering(byRank);
+  std::ostringstream o;
+  o << "{\"ok\":" << (dl.ok ? 1 : 0) << ",\"coll\":" << dl.coll;
+  if (dl.ok) {
+    o << ",\"classes\":[";
+    for (size_t k = 0; k < dl.order.size(); k++) {
+      o << (k ? "," : "") << "[";
+      for (size_t r = 0; r < dl.order[k].size(); r++) {
+        o << (r ? "," : "") << "[";
+        for (size_t i = 0; i < dl.order[k][r].size(); i++) o << (i ? "," : "") << dl.order[k][r][i];
+        o << "]";
+      }
+      o << "]";
+    }
+    o << "],\"chunkClass\":[";
+    for (size_t c = 0; c < dl.chunkClass.size(); c++) o << (c ? "," : "") << dl.chunkClass[c];
+    o << "]";
+  } else {
+    o << ",\"why\":\"" << dl.why << "\"";
+  }
+  o << "}";
+  return putOut(o.str(), out, outLen);
+}
+
 // the collective the fold kernel would run for this fallback plan (plan.cc: makeFlatTreePlan;
 // kRingAllReduce / kRingReduceScatter / kRingAllGather), 0 when the call keeps the ring / chain
 static int flatOf(const CallDesc& c, const Knobs& k, Plan rp) {

@@ -47,6 +47,7 @@ constexpr int kMaxFlatSubs = 128;
 constexpr int kFoldPacksPerWg = 512;   // flat tree: a fold workgroup per 512 packs (8 KiB) of the call
 constexpr int kMaxFoldClasses = 16;    // lowered schedules (lower.cc): fold orders per schedule
 constexpr int kMaxFoldChunks = 1024;   // lowered schedules with several orders: chunks per loop
+constexpr int kMaxDirectClasses = 256; // the direct form (DirectLowering): fold orders (a 32-ring schedule: 256)
 
 // Device trace event (mscclAmdTraceRead).
 struct TraceEvent {
@@ -236,6 +237,7 @@ struct RankWork {
   uint32_t tpMagic;
   uint8_t tpSh1, tpSh2;
   uint16_t tpStepPacks;         // packs per FIFO step (at most a slot's): the FIFO footprint in flight
+  int16_t directRank;           // the direct form (mscclDirectKernel): this work's rank (the launch holds every rank)
 #ifdef MSCCL_RANKWORK_TEST_PAD
   // a deliberate layout split (tools/varbuild.sh's guard test): a kernel object built with this
   // define has a larger RankWork, so it reads every rank's entry after the first of the launch
@@ -296,6 +298,8 @@ LaunchFn getPairLaunchFn(int dtype, int redop);
 // The two-phase fold (mscclTwoPhaseKernel, interpreter.h: runTwoPhase): a lowered schedule's
 // large calls, LL, Sum..Min
 LaunchFn getTwoPhaseLaunchFn(int dtype, int redop);
+// The direct form of a Simple schedule (mscclDirectKernel, interpreter.h: DirectRunner), Sum..Min
+LaunchFn getDirectLaunchFn(int dtype, int redop);
 // the name of the first type whose kernel object was built with another RankWork layout, or null
 const char* kernelLayoutMismatch();
 // One-thread kernel that writes the GPU clock (s_memrealtime) to *hostWord (host-mapped):

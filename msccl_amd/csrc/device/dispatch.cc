@@ -3,7 +3,8 @@
 
 namespace msccl {
 #define MSCCL_DECL(N) extern LaunchFn N[6][3]; extern LaunchFn N##_small[2][4]; extern LaunchFn N##_fold[4]; \
-  extern LaunchFn N##_pair[4]; extern LaunchFn N##_two[4]; extern OneRankFn N##_one; extern const uint32_t N##_layout;
+  extern LaunchFn N##_pair[4]; extern LaunchFn N##_two[4]; extern LaunchFn N##_direct[4]; extern OneRankFn N##_one; \
+  extern const uint32_t N##_layout;
 MSCCL_DECL(gLaunch_i8)
 MSCCL_DECL(gLaunch_u8)
 MSCCL_DECL(gLaunch_i32)
@@ -53,6 +54,15 @@ LaunchFn getPairLaunchFn(int dtype, int devOp) {
 LaunchFn getTwoPhaseLaunchFn(int dtype, int devOp) {
   LaunchFn* tabs[10] = {gLaunch_i8_two, gLaunch_u8_two, gLaunch_i32_two, gLaunch_u32_two, gLaunch_i64_two,
                         gLaunch_u64_two, gLaunch_f16_two, gLaunch_f32_two, gLaunch_f64_two, gLaunch_bf16_two};
+  if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
+  return tabs[dtype][devOp];
+}
+
+// the direct form (mscclDirectKernel): Simple schedules, devOp Sum..Min
+LaunchFn getDirectLaunchFn(int dtype, int devOp) {
+  LaunchFn* tabs[10] = {gLaunch_i8_direct, gLaunch_u8_direct, gLaunch_i32_direct, gLaunch_u32_direct,
+                        gLaunch_i64_direct, gLaunch_u64_direct, gLaunch_f16_direct, gLaunch_f32_direct,
+                        gLaunch_f64_direct, gLaunch_bf16_direct};
   if (dtype < 0 || dtype > 9 || devOp < 0 || devOp > 3) return nullptr;
   return tabs[dtype][devOp];
 }

@@ -1706,7 +1706,7 @@ struct Interp {
   // at once own disjoint packs: in-place calls are safe.  The three phases are software-pipelined
   // over the steps (below); no workgroup waits on a peer's step the peer has not reached, so the
   // loop cannot deadlock.
-  __device__ __forceinline__ uint32_t divQ(uint32_t m, uint32_t magic, int sh1, int sh2) const {
+  static __device__ __forceinline__ uint32_t divQ(uint32_t m, uint32_t magic, int sh1, int sh2) {
     const uint32_t t = __umulhi(m, magic);
     return (t + ((m - t) >> sh1)) >> sh2;
   }
@@ -2331,6 +2331,157 @@ __global__ void __launch_bounds__(kNT, 1) mscclTwoPhaseKernel(const LaunchArgsN<
   Interp<T, OP, pLL> it;
   it.sh = &sh;
   it.runTwoPhase(w, b - w.blockBase, &fs);
+}
+
+
+// ---------------------------------------------------------------- the direct form (Simple)
+// A Simple schedule's call when every rank of the communicator is in this launch (lower.h:
+// DirectLowering; enqueue.cc: launchGroup).  The reference's P2P direct mode lets a sender write
+// straight into the receiver's buffer inside one process (prims_simple.h:75-128, 500-560, the
+// pointer travelling through ptrExchange, comm.h:39); within one fused launch every rank's buffers
+// are addressable and ready when it starts, so no FIFO, flag or pointer exchange is needed: the
+// launch's argument block holds every rank's RankWork, in rank order.  Rank r's workgroups
+//   AllGather:     copy r's input to block r of every rank's output (read once, written n times);
+//   ReduceScatter: fold block r of every rank's input in the schedule's order of the pack's
+//                  chunk class and store r's output;
+//   AllReduce:     fold their share of every rank's input (the same order on every rank) and
+//                  store the result into every rank's output.
+// A lane reads every operand of a pack before it writes that pack anywhere, and no other lane
+// of the launch reads or writes it: in-place AllReduce calls are safe.
+struct alignas(16) DirectShared {
+  const void* rankBuf[kMaxLaunchRanks];                // every rank's input, by rank
+  uint8_t perm[kMaxDirectClasses][kMaxLaunchRanks];    // per class: the ranks in fold order
+  uint8_t chunkClass[kMaxFoldChunks];                  // per output chunk: its class
+};
+
+template <typename T, int OP>
+struct DirectRunner : Interp<T, OP, pSimple> {
+  using I = Interp<T, OP, pSimple>;
+  using I::PE;
+  using F = typename I::F;
+  static constexpr int UD = 2;  // packs per lane per pass (n loads each in flight)
+  // pack B of a block of n elements at a per-lane address (the rank whose operand a lane loads
+  // follows its pack's chunk class, so a wave's lanes may read different ranks' buffers: no
+  // wave-uniform buffer descriptor)
+  static __device__ __forceinline__ u32x4 ldPackLane(const T* base, int B, int n) {
+    const int e0 = B * PE;
+    const int ne = n - e0;
+    if (ne >= PE && (((uintptr_t)base & 15) == 0)) return *(const u32x4*)(base + e0);
+    T v[PE];
+#pragma unroll
+    for (int i = 0; i < PE; i++) {
+      if (i < ne) v[i] = base[e0 + i];
+      else __builtin_memset(&v[i], 0, sizeof(T));
+    }
+    u32x4 o;
+    __builtin_memcpy(&o, v, 16);
+    return o;
+  }
+  template <int R>
+  __device__ __forceinline__ void run(const LaunchArgsN<R>& args, const RankWork& w, int wg, DirectShared* fs) {
+    I& it = *this;
+    it.tid = threadIdx.x;
+    const int tid = it.tid;
+    const int n = args.nRanks;
+    const int me = w.directRank;
+    const int mode = w.ringColl;
+    const int64_t count = w.sizePerChunk;  // elements of one rank block (AG: input, RS: output, AR: buffer)
+    const int wgs = w.split;
+    const int Q = w.foldChunkPacks;        // packs per chunk (RS / AR), for the chunk's class
+    const uint32_t magic = w.tpMagic;
+    const int sh1 = w.tpSh1, sh2 = w.tpSh2;
+    // the fold orders of this rank (image: transfer 0 the orders, ranks per class; transfer 1 the
+    // class of every chunk), read from the image in global memory into LDS
+    if (mode != kRingAllGather) {
+      const char* img = (const char*)w.images;
+      const DevTbHeader* hd = (const DevTbHeader*)img;
+      const DevTransfer* tr0 = (const DevTransfer*)(img + sizeof(DevTbHeader));
+      const int16_t* reds = (const int16_t*)(tr0 + hd->nsteps) + 2 * hd->ndeps;
+      const int nOrd = tr0[0].srcoff * n, p0r = tr0[0].redPtr, nCh = tr0[1].srcoff, p1r = tr0[1].redPtr;
+      for (int i = tid; i < nOrd; i += kNT) fs->perm[i / n][i % n] = (uint8_t)reds[p0r + i];
+      for (int i = tid; i < nCh; i += kNT) fs->chunkClass[i] = (uint8_t)reds[p1r + i];
+    }
+    for (int q = 0; q < n; q++)  // (a uniform index: kernel-argument loads stay scalar)
+      if (tid == q) fs->rankBuf[q] = args.w[q].sendbuff;  // the per-lane rank choice below reads LDS
+    __syncthreads();
+    const int64_t npkAll = (count + PE - 1) / PE;
+    // this workgroup's packs: AG / RS the whole rank block, AR this rank's share of it
+    int64_t lo = 0, hi = npkAll;
+    if (mode == kRingAllReduce) {
+      lo = npkAll * me / n;
+      hi = npkAll * (me + 1) / n;
+    }
+    const int64_t span = hi - lo;
+    const int64_t p0 = lo + span * wg / wgs, p1 = lo + span * (wg + 1) / wgs;
+    const int64_t rsOff = mode == kRingReduceScatter ? (int64_t)me * count : 0;  // RS: block me of every input
+    for (int64_t base = p0; base < p1; base += (int64_t)kNT * UD) {
+      int B[UD];
+      bool act[UD];
+#pragma unroll
+      for (int u = 0; u < UD; u++) {
+        const int64_t b = base + tid + (int64_t)u * kNT;
+        act[u] = b < p1;
+        B[u] = act[u] ? (int)b : 0;
+      }
+      if (mode == kRingAllGather) {
+        const T* src = (const T*)args.w[me].sendbuff;
+        const __amdgpu_buffer_rsrc_t srs = makeRsrc(src);
+        const bool sv = I::aligned16(src);
+        u32x4 v[UD];
+#pragma unroll
+        for (int u = 0; u < UD; u++) v[u] = act[u] ? it.loadPack(srs, sv, B[u], (int)count) : (u32x4){0, 0, 0, 0};
+        for (int q = 0; q < n; q++) {
+          T* dst = (T*)args.w[q].recvbuff + (int64_t)me * count;
+          const __amdgpu_buffer_rsrc_t drs = makeRsrc(dst);
+          const bool dv = I::aligned16(dst);
+#pragma unroll
+          for (int u = 0; u < UD; u++)
+            if (act[u]) it.storePack(drs, dv, B[u], (int)count, v[u]);
+        }
+        continue;
+      }
+      // RS / AR: every rank's pack, folded in the order of the pack's chunk class
+      u32x4 acc[UD];
+      const uint8_t* pm[UD];
+#pragma unroll
+      for (int u = 0; u < UD; u++) {
+        const uint32_t c = Q > 0 ? (uint32_t)I::divQ((uint32_t)B[u], magic, sh1, sh2) : 0;
+        pm[u] = fs->perm[fs->chunkClass[c]];
+      }
+      for (int j = 0; j < n; j++) {
+        u32x4 v[UD];
+#pragma unroll
+        for (int u = 0; u < UD; u++) {
+          const int q = pm[u][j];
+          v[u] = act[u] ? ldPackLane((const T*)fs->rankBuf[q] + rsOff, B[u], (int)count) : (u32x4){0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < UD; u++) acc[u] = j == 0 ? v[u] : F::pack(acc[u], v[u]);
+      }
+      const int nOut = mode == kRingAllReduce ? n : 1;
+      for (int q0 = 0; q0 < nOut; q0++) {
+        const int q = mode == kRingAllReduce ? q0 : me;
+        T* dst = (T*)args.w[q].recvbuff;
+        const __amdgpu_buffer_rsrc_t drs = makeRsrc(dst);
+        const bool dv = I::aligned16(dst);
+#pragma unroll
+        for (int u = 0; u < UD; u++)
+          if (act[u]) it.storePack(drs, dv, B[u], (int)count, acc[u]);
+      }
+    }
+  }
+};
+
+// The direct form (DirectRunner): every rank of the communicator in this launch, RankWork in rank
+// order; rank r owns workgroups [blockBase, blockBase + nBlocks).
+template <typename T, int OP, int R>
+__global__ void __launch_bounds__(kNT, 2) mscclDirectKernel(const LaunchArgsN<R> args) {
+  __shared__ DirectShared ds;
+  const int b = blockIdx.x;
+  const RankWork& w = rankWorkOf(args, b);
+  DirectRunner<T, OP> it;
+  it.sh = nullptr;  // no program image in LDS
+  it.run(args, w, b - w.blockBase, &ds);
 }
 
 }  // namespace msccl

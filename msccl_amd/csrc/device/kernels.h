@@ -94,6 +94,31 @@ int launchTwoPhaseKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
   return hipGetLastError() == hipSuccess ? 0 : 1;
 }
 
+// the direct form (mscclDirectKernel, Simple schedules, Sum..Min): every rank of the communicator in
+// the launch, RankWork in rank order
+template <typename T, int OP>
+int launchDirectKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
+  constexpr int RC = kCompactLaunchRanks;
+  if (gridBlocks == kQueryResidency) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mscclDirectKernel<T, OP, kMaxLaunchRanks>, kNT, 0) != hipSuccess)
+      return 0;
+    return n;
+  }
+  if (gridBlocks < args.nRanks) return 1;
+  if (args.nRanks <= RC) {
+    LaunchArgsN<RC> a;
+    a.nRanks = args.nRanks;
+    a.pad = 0;
+    for (int r = 0; r < RC; r++) a.w[r] = args.w[r];
+    hipLaunchKernelGGL((mscclDirectKernel<T, OP, RC>), dim3(gridBlocks), dim3(kNT), 0, (hipStream_t)stream, a);
+  } else {
+    hipLaunchKernelGGL((mscclDirectKernel<T, OP, kMaxLaunchRanks>), dim3(gridBlocks), dim3(kNT), 0,
+                       (hipStream_t)stream, args);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : 1;
+}
+
 // the pair kernel (mscclPairKernel, LL, Sum..Min): same contract as launchSmallKernel
 template <typename T, int OP>
 int launchPairKernel(const LaunchArgs& args, int gridBlocks, void* stream) {
@@ -161,6 +186,8 @@ int launchOneRankScale(const void* src, void* dst, size_t n, uint64_t arg, int a
                              launchPairKernel<T, kMin>};                                                   \
   LaunchFn NAME##_two[4] = {launchTwoPhaseKernel<T, kSum>, launchTwoPhaseKernel<T, kProd>,                  \
                             launchTwoPhaseKernel<T, kMax>, launchTwoPhaseKernel<T, kMin>};                 \
+  LaunchFn NAME##_direct[4] = {launchDirectKernel<T, kSum>, launchDirectKernel<T, kProd>,                   \
+                               launchDirectKernel<T, kMax>, launchDirectKernel<T, kMin>};                  \
   extern const uint32_t NAME##_layout = kWorkLayout;
 #define MSCCL_DEFINE_TABLE(NAME, T)                                                                        \
   LaunchFn NAME[6][3] = {MSCCL_OPS_0_3(T),                                                                 \

@@ -255,6 +255,54 @@ RankWork makeFlatWork(Planned& p) {
   return w;
 }
 
+// The direct form of a Simple schedule (interpreter.h: DirectRunner; lower.h: DirectLowering):
+// launchGroup runs it when every rank of the communicator is in the launch.  No connection, flag
+// or epoch is touched (a later interpreted call of the schedule finds them as the last one left
+// them).  Workgroups per rank: the Simple budget (512 per GPU) over the ranks, at most
+// kMaxFlatSubs, and no more than keep two packs per lane.
+RankWork makeDirectWork(Planned& p) {
+  ncclComm* comm = p.op.comm;
+  const int g = p.plan.algoIndex;
+  const DevAlgoHost& da = comm->directAlgos[g];
+  const int coll = comm->algoDirect[g].coll;
+  const int n = comm->nRanks;
+  RankWork w;
+  memset(&w, 0, sizeof(w));
+  w.sendbuff = p.op.sendbuff;
+  w.recvbuff = p.op.recvbuff;
+  w.comm = comm->dComm;
+  w.images = da.dImages;
+  w.tbStride = da.tbStride;
+  w.timeoutTicks = comm->timeoutTicks;
+  w.llFlagMask = comm->llFlagMask;
+  w.llCleanMask = comm->llCleanMask;
+  w.refNthreads = (int16_t)p.plan.refNthreads;
+  w.ringColl = (uint8_t)(coll == kAllGather ? kRingAllGather : coll == kReduceScatter ? kRingReduceScatter : kRingAllReduce);
+  w.sizePerChunk = p.plan.count;  // one rank block: AG input bytes, RS output elements, AR elements
+  const int64_t pe = 16 / refTypeSize(p.plan.dtype);
+  const int64_t packs = (p.plan.count + pe - 1) / pe;
+  const int64_t share = coll == kAllReduce ? (packs + n - 1) / n : packs;
+  const int64_t perWg = (int64_t)kNT * 2;
+  const int wgs = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)512 / n, (int64_t)kMaxFlatSubs,
+                                                                (share + perWg - 1) / perWg}));
+  w.split = (uint8_t)wgs;
+  w.nBlocks = (int16_t)wgs;
+  w.merge = 1;
+  w.maxAllowedCount = 1;
+  const uint32_t d = (uint32_t)p.plan.directChunkPacks;  // packs per output chunk (0: one class)
+  w.foldChunkPacks = (int32_t)d;
+  if (d > 0) {
+    const int l = d <= 1 ? 0 : 32 - __builtin_clz(d - 1);  // the two-phase fold's division (makeFlatWork)
+    w.tpMagic = (uint32_t)((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d + 1);
+    w.tpSh1 = (uint8_t)std::min(l, 1);
+    w.tpSh2 = (uint8_t)std::max(l - 1, 0);
+  }
+  w.directRank = (int16_t)comm->rank;
+  w.launchSeq = comm->workIndex++;
+  comm->last = {g, p.plan.proto, wgs, 1, 0, 0, w.nBlocks};
+  return w;
+}
+
 RankWork makeWork(Planned& p) {
   if (p.plan.ringColl == kTreeFlat) return makeFlatWork(p);
   if (p.plan.ringColl) return makeRingWork(p);
@@ -400,16 +448,36 @@ bool smallEligible(const Planned& p, const RankWork& w) {
   return p.plan.sizePerChunk * chunks * refTypeSize(p.plan.dtype) <= (1ll << 30);  // runSmall's 32-bit offsets
 }
 
+// The direct form runs when every op of the launch may (Plan::directOk: the same schedule) and the
+// launch holds every rank of one clique (ncclComm::clique) once: then all of them are in this
+// launch, whose start follows every rank's stream, and the argument block, in rank order, gives
+// every rank's buffers.  The decision is the same for every rank (they are all here).
+bool directLaunch(std::vector<Planned*>& ps) {
+  const ncclComm* c0 = ps[0]->op.comm;
+  if (c0->clique == 0 || (int)ps.size() != c0->nRanks) return false;
+  std::vector<bool> seen(c0->nRanks, false);
+  for (const Planned* p : ps) {
+    const ncclComm* c = p->op.comm;
+    if (!p->plan.directOk || c->clique != c0->clique || p->plan.algoIndex != ps[0]->plan.algoIndex ||
+        p->op.coll != ps[0]->op.coll || p->op.count != ps[0]->op.count || seen[c->rank])
+      return false;
+    seen[c->rank] = true;
+  }
+  std::sort(ps.begin(), ps.end(), [](const Planned* a, const Planned* b) { return a->op.comm->rank < b->op.comm->rank; });
+  return true;
+}
+
 ncclResult_t launchGroup(std::vector<Planned*>& ps) {
+  const bool direct = directLaunch(ps);  // (sorts ps by rank when true)
   ncclComm* c0 = ps[0]->op.comm;
   int dev = c0->cudaDev;
   hipStream_t primary = ps[0]->op.stream;
   LaunchArgs args;
   memset(&args, 0, sizeof(args));
   int blocks = 0;
-  bool small = true;
+  bool small = !direct;
   for (size_t i = 0; i < ps.size(); i++) {
-    RankWork w = makeWork(*ps[i]);
+    RankWork w = direct ? makeDirectWork(*ps[i]) : makeWork(*ps[i]);
     w.blockBase = (int16_t)blocks;
     blocks += w.nBlocks;
     args.w[i] = w;
@@ -429,7 +497,7 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   const Planned& p0 = *ps[0];
   // a launch group holds flat works of one lowering mode only, or none (executeOps keys launches
   // on it): the fold, the pair kernel on the flat connections, or the two-phase fold
-  const bool flatWork = p0.plan.ringColl == kTreeFlat;
+  const bool flatWork = !direct && p0.plan.ringColl == kTreeFlat;
   const bool fold = flatWork && p0.plan.lowerMode == kLowerFold;
   const bool lowPair = flatWork && p0.plan.lowerMode == kLowerPair;
   const bool two = flatWork && p0.plan.lowerMode == kLowerTwoPhase;
@@ -450,8 +518,9 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
   }
   // (the lowered pair runs the pair kernel whatever MSCCL_AMD_PAIR_KERNEL says: both ends of its
   // flat connections run it, the plan being the same on every rank)
-  pair = pair || lowPair;
-  LaunchFn fn = fold ? getFoldLaunchFn(p0.plan.dtype, p0.op.devOp)
+  pair = !direct && (pair || lowPair);
+  LaunchFn fn = direct ? getDirectLaunchFn(p0.plan.dtype, p0.op.devOp)
+                : fold ? getFoldLaunchFn(p0.plan.dtype, p0.op.devOp)
                 : two ? getTwoPhaseLaunchFn(p0.plan.dtype, p0.op.devOp)
                 : pair ? getPairLaunchFn(p0.plan.dtype, p0.op.devOp)
                 : small ? getSmallLaunchFn(p0.plan.dtype, p0.op.devOp, set)
@@ -462,7 +531,7 @@ ncclResult_t launchGroup(std::vector<Planned*>& ps) {
     p->op.comm->last.small = flatWork ? 2 : small ? 1 : 0;
     p->op.comm->last.set = small && !flatWork ? set : 0;
     p->op.comm->last.pair = pair ? 1 : 0;
-    p->op.comm->last.kernel = fold ? 2 : two ? 4 : pair ? 3 : small ? 1 : 0;
+    p->op.comm->last.kernel = direct ? 5 : fold ? 2 : two ? 4 : pair ? 3 : small ? 1 : 0;
   }
   if (!fn) { WARN("MSCCL: no kernel for type %d op %d proto %d", p0.plan.dtype, p0.op.devOp, p0.plan.proto); return ncclInvalidArgument; }
   {

@@ -46,6 +46,27 @@ ncclResult_t loadAlgos(ncclComm* comm) {
 // then keeps a lowering only where every rank reached it (applySplits).
 void analyzeLowering(ncclComm* comm) {
   comm->algoFold.assign(comm->algos.size(), ncclComm::FoldProgram());
+  comm->algoDirect.assign(comm->algos.size(), ncclComm::DirectProgram());
+  if (comm->knobs.direct && lowerOffered()) {
+    // the direct form of Simple schedules (lower.h: DirectLowering); used only when every rank of
+    // the communicator runs in one launch (enqueue.cc: launchGroup)
+    for (size_t g = 0; g < comm->algos.size(); g++) {
+      const Algorithm& a = comm->algos[g];
+      if (!a.valid || a.proto != kProtoSimple || a.path.empty() || a.ngpus != comm->nRanks ||
+          !(a.coll == kAllReduce || a.coll == kReduceScatter || a.coll == kAllGather))
+        continue;
+      const DirectLowering dl = directScheduleFile(a.path, comm->nRanks);
+      if (dl.ok) {
+        ncclComm::DirectProgram& d = comm->algoDirect[g];
+        d.coll = dl.coll;
+        d.chunkClass = dl.chunkClass;
+        for (auto& perRank : dl.order) d.order.push_back(perRank[comm->rank]);
+      }
+      INFO(kSubInit, "MSCCL: algorithm %s %s", a.name.c_str(),
+           dl.ok ? "has a direct form (ranks in one launch write each other's buffers)"
+                 : ("has no direct form (" + dl.why + ")").c_str());
+    }
+  }
   if (!comm->knobs.lower || !flatEnabled(comm) || !lowerOffered()) return;
   for (size_t g = 0; g < comm->algos.size(); g++) {
     const Algorithm& a = comm->algos[g];
@@ -145,6 +166,7 @@ SplitRecord makeSplitRecord(ncclComm* comm) {
     s.lowered[a] = a < comm->algoFold.size() && !comm->algoFold[a].order.empty()
                        ? (comm->algoFold[a].owner.empty() ? 1 : 3)
                        : 0;
+    if (a < comm->algoDirect.size() && comm->algoDirect[a].coll >= 0) s.lowered[a] |= 4;
     const std::vector<FuseCandidate> fc = fusableTbs(comm->algos[a]);
     s.pairShape[a] = comm->knobs.fuse && pairFormOf(comm->algos[a], fc).src >= 0;
     s.pairRun[a] = s.pairShape[a] && comm->knobs.pairKernel;
@@ -189,6 +211,7 @@ static std::string knobDiff(const Knobs& a, const Knobs& b) {
   add(a.lowerLarge != b.lowerLarge, "MSCCL_AMD_LOWER_LARGE");
   add(a.forceRemote != b.forceRemote, "MSCCL_AMD_FORCE_REMOTE");
   add(a.twoPhaseStep != b.twoPhaseStep, "MSCCL_AMD_TWO_PHASE_STEP");
+  add(a.direct != b.direct, "MSCCL_AMD_DIRECT");
   return out.empty() ? "(unnamed field)" : out;
 }
 
@@ -259,6 +282,10 @@ ncclResult_t applySplits(ncclComm* comm, const std::vector<SplitRecord>& recs) {
     for (auto& r : recs)
       if ((int)a >= r.nAlgos || (r.lowered[a] & 2) == 0) comm->algoFold[a].owner.clear();
   }
+  // the direct form likewise
+  for (size_t a = 0; a < comm->algoDirect.size() && a < (size_t)kMaxAlgos; a++)
+    for (auto& r : recs)
+      if ((int)a >= r.nAlgos || (r.lowered[a] & 4) == 0) comm->algoDirect[a] = ncclComm::DirectProgram();
   // Lowered large calls (plan.cc: lowerLargePlan): 2 ranks run the pair kernel on the flat
   // connections, more ranks the two-phase fold, each with up to flatSubs workgroups per rank and
   // one flat sub-connection per workgroup: one workgroup per CU over the GPU's co-resident ranks
@@ -337,12 +364,17 @@ ncclResult_t commFinish(ncclComm* comm) {
     comm->foldClasses[a] = (int)comm->algoFold[a].order.size();
     comm->foldTwoPhase[a] = comm->algoFold[a].owner.empty() ? 0 : 1;
   }
+  comm->directClasses.assign(comm->algos.size(), 0);
+  for (size_t a = 0; a < comm->algoDirect.size() && a < comm->algos.size(); a++)
+    if (comm->algoDirect[a].coll >= 0) comm->directClasses[a] = std::max<int>(1, (int)comm->algoDirect[a].order.size());
   PlanContext& pc = comm->planCtx;
   pc.algos = &comm->algos;
   pc.regs = &comm->regs;
   pc.knobs = &comm->knobs;
   pc.foldClasses = &comm->foldClasses;
   pc.foldTwoPhase = &comm->foldTwoPhase;
+  pc.directClasses = &comm->directClasses;
+  pc.oneLaunch = comm->clique != 0;
   pc.flat = flatEnabled(comm);
   pc.ringFallback = comm->ringFallback;
   pc.scratchSize = comm->scratchSize;
@@ -465,6 +497,8 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
     if (d.dImages) hipFree(d.dImages);  // their connection records are comm->ringSend / ringRecv
   for (auto& d : comm->foldAlgos)
     if (d.dImages) hipFree(d.dImages);  // the flat connections (comm->flatSend / flatRecv)
+  for (auto& d : comm->directAlgos)
+    if (d.dImages) hipFree(d.dImages);  // no connections
   if (comm->ringSend) hipFree(comm->ringSend);
   if (comm->ringRecv) hipFree(comm->ringRecv);
   if (comm->treeSend) hipFree(comm->treeSend);
@@ -560,6 +594,11 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   }
   std::vector<ncclComm*> cs(ndev);
   ncclResult_t res = ncclSuccess;
+  // every rank on one device: one clique, whose group calls are one fused launch (comm.h: clique)
+  bool oneDevice = ndev > 1;
+  for (int i = 1; i < ndev && oneDevice; i++) oneDevice = (devlist ? devlist[i] : i) == (devlist ? devlist[0] : 0);
+  static std::atomic<uint64_t> cliques{0};
+  const uint64_t clique = oneDevice ? ++cliques : 0;
   for (int i = 0; i < ndev && res == ncclSuccess; i++) {
     int dev = devlist ? devlist[i] : i;
     if (dev < 0 || dev >= ndevices) {
@@ -571,6 +610,7 @@ ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
     c->rank = i;
     c->nRanks = ndev;
     c->cudaDev = dev;
+    c->clique = clique;
     cs[i] = c;
     res = commLocalSetup(c);
   }

@@ -91,33 +91,22 @@ struct TbState {
 
 }  // namespace
 
-FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
-  FoldLowering out;
+// Runs every rank's program on chunk expressions (the semantics in the header comment; `re` in the
+// protocol's order: LL / LL128 acc = d, acc = fn(acc, s_i) (prims_ll.h:347-362); Simple
+// acc = s_0, acc = fn(acc, s_i), then fn(acc, d) (prims_simple.h:258-263, the big-call path)).
+// inB[r] holds leaf(r, c) for c < cin, outB[r] cout undefined chunks (the output aliases the input
+// of an in-place AllReduce).  Returns "" or why the schedule cannot be followed.
+static std::string symRun(const std::vector<Algorithm>& byRank, int cin, int cout, bool simpleOrder, Exprs& ex,
+                          std::vector<std::vector<int>>& inB, std::vector<std::vector<int>>& outB) {
   const int n = (int)byRank.size();
-  auto fail = [&](const std::string& why) {
-    out.ok = false;
-    out.why = why;
-    out.order.clear();
-    out.chunkClass.clear();
-    return out;
-  };
-  if (n < 2 || n > kMaxReduceFusion) return fail("ranks outside 2..16");
-  const Algorithm& a0 = byRank[0];
-  const int C = a0.nchunksPerLoop;
-  if (C <= 0) return fail("no chunks");
-  for (const Algorithm& a : byRank) {
-    if (!a.valid || a.coll != kAllReduce) return fail("not a valid AllReduce schedule");
-    if (a.proto != kProtoLL) return fail("protocol is not LL");
-    if (a.nchunksPerLoop != C || a.inPlace != a0.inPlace) return fail("ranks disagree on the loop shape");
-  }
-  Exprs ex;
-  // buffers per rank: input, output (aliases the input in place), scratch
-  std::vector<std::vector<int>> inB(n), outB(n), scrB(n);
+  std::vector<std::vector<int>> scrB(n);
+  inB.assign(n, {});
+  outB.assign(n, {});
   for (int r = 0; r < n; r++) {
     const Algorithm& a = byRank[r];
-    inB[r].assign(std::max(C, a.nInputChunks), Exprs::kUndef);
-    for (int c = 0; c < (int)inB[r].size(); c++) inB[r][c] = c < C ? ex.leaf(r, c, C) : Exprs::kUndef;
-    if (!a.inPlace) outB[r].assign(std::max(C, a.nOutputChunks), Exprs::kUndef);
+    inB[r].assign(std::max(cin, a.nInputChunks), Exprs::kUndef);
+    for (int c = 0; c < (int)inB[r].size(); c++) inB[r][c] = c < cin ? ex.leaf(r, c, cin) : Exprs::kUndef;
+    if (!a.inPlace) outB[r].assign(std::max(cout, a.nOutputChunks), Exprs::kUndef);
     scrB[r].assign(std::max(0, a.nScratchChunks), Exprs::kUndef);
   }
   auto buf = [&](int r, int id) -> std::vector<int>* {
@@ -140,12 +129,12 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
         const ThreadBlock& tb = a.tbs[b];
         TbState& s = st[r][b];
         while (s.pc < tb.transfers.size()) {
-          if (++guard > (size_t)1 << 24) return fail("schedule too large to analyse");
+          if (++guard > (size_t)1 << 24) return "schedule too large to analyse";
           const Transfer& t = tb.transfers[s.pc];
           bool ready = true;
           for (int d = 0; d < t.numDeps && ready; d++) {
             const int db = tb.depBid[t.depPtr + d], ds = tb.depStep[t.depPtr + d];
-            if (db < 0 || db >= a.nBlocks) return fail("dependency on a missing thread block");
+            if (db < 0 || db >= a.nBlocks) return "dependency on a missing thread block";
             ready = st[r][db].published >= ds;
           }
           const bool recv = t.type == kRecv || t.type == kRecvCopySend || t.type == kRecvReduceSend ||
@@ -154,12 +143,12 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
                             t.type == kRecvReduceCopySend;
           std::vector<std::vector<int>>* in = nullptr;
           if (ready && recv) {
-            if (tb.recvpeer < 0) return fail("receive without a peer");
+            if (tb.recvpeer < 0) return "receive without a peer";
             in = &fifo[std::make_tuple((int)tb.channel, (int)tb.recvpeer, r)];
             ready = !in->empty();
           }
           if (!ready) break;
-          if (send && tb.sendpeer < 0) return fail("send without a peer");
+          if (send && tb.sendpeer < 0) return "send without a peer";
           const int cnt = t.count;
           std::vector<int>* src = buf(r, t.srcbuf);
           std::vector<int>* dst = buf(r, t.dstbuf);
@@ -176,7 +165,7 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
           if (recv) {
             msg = in->front();
             in->erase(in->begin());
-            if ((int)msg.size() != cnt) return fail("receive count differs from the matching send");
+            if ((int)msg.size() != cnt) return "receive count differs from the matching send";
           }
           std::vector<int> outMsg;
           switch (t.type) {
@@ -185,19 +174,19 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
               break;
             case kRecv:
               for (int c = 0; c < cnt; c++)
-                if (!wr(dst, t.dstoff + c, msg[c])) return fail("receive into a missing chunk");
+                if (!wr(dst, t.dstoff + c, msg[c])) return "receive into a missing chunk";
               break;
             case kRecvCopySend:
               for (int c = 0; c < cnt; c++)
-                if (!wr(dst, t.dstoff + c, msg[c])) return fail("receive into a missing chunk");
+                if (!wr(dst, t.dstoff + c, msg[c])) return "receive into a missing chunk";
               outMsg = msg;
               break;
             case kRecvReduceSend:
             case kRecvReduceCopy:
             case kRecvReduceCopySend:
               for (int c = 0; c < cnt; c++) {
-                const int v = ex.op(msg[c], rd(src, t.srcoff + c), r);  // fn(peer, local)
-                if (t.type != kRecvReduceSend && !wr(dst, t.dstoff + c, v)) return fail("write to a missing chunk");
+                const int v = ex.op(msg[c], rd(src, t.srcoff + c), r);  // fn(peer, local) == fn(local, peer)
+                if (t.type != kRecvReduceSend && !wr(dst, t.dstoff + c, v)) return "write to a missing chunk";
                 if (t.type != kRecvReduceCopy) outMsg.push_back(v);
               }
               break;
@@ -205,18 +194,25 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
               std::vector<int> v;
               for (int c = 0; c < cnt; c++) v.push_back(rd(src, t.srcoff + c));
               for (int c = 0; c < cnt; c++)
-                if (!wr(dst, t.dstoff + c, v[c])) return fail("copy to a missing chunk");
+                if (!wr(dst, t.dstoff + c, v[c])) return "copy to a missing chunk";
               break;
             }
             case kReduce:
               for (int c = 0; c < cnt; c++) {
-                int acc = rd(dst, t.dstoff + c);
-                for (int j = 0; j < t.numReds; j++) acc = ex.op(acc, rd(src, tb.redSrcOff[t.redPtr + j] + c), r);
-                if (!wr(dst, t.dstoff + c, acc)) return fail("reduce into a missing chunk");
+                int acc;
+                if (simpleOrder) {
+                  acc = rd(src, tb.redSrcOff[t.redPtr] + c);
+                  for (int j = 1; j < t.numReds; j++) acc = ex.op(acc, rd(src, tb.redSrcOff[t.redPtr + j] + c), r);
+                  acc = ex.op(acc, rd(dst, t.dstoff + c), r);
+                } else {
+                  acc = rd(dst, t.dstoff + c);
+                  for (int j = 0; j < t.numReds; j++) acc = ex.op(acc, rd(src, tb.redSrcOff[t.redPtr + j] + c), r);
+                }
+                if (!wr(dst, t.dstoff + c, acc)) return "reduce into a missing chunk";
               }
               break;
             default:
-              return fail("transfer type without a lowering (res-add or unknown)");
+              return "transfer type without a lowering (res-add or unknown)";
           }
           if (send) fifo[std::make_tuple((int)tb.channel, r, (int)tb.sendpeer)].push_back(outMsg);
           if (t.numDeps > 0) s.step += t.numDeps - 1;
@@ -231,68 +227,107 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
   }
   for (int r = 0; r < n; r++)
     for (int b = 0; b < byRank[r].nBlocks; b++)
-      if (st[r][b].pc < byRank[r].tbs[b].transfers.size()) return fail("schedule does not complete");
+      if (st[r][b].pc < byRank[r].tbs[b].transfers.size()) return "schedule does not complete";
   for (auto& kv : fifo)
-    if (!kv.second.empty()) return fail("unconsumed FIFO messages");
+    if (!kv.second.empty()) return "unconsumed FIFO messages";
+  for (int r = 0; r < n; r++)
+    if (!byRank[r].inPlace)
+      for (int c = 0; c < cin; c++)
+        if (inB[r][c] != ex.leaf(r, c, cin)) return "an out-of-place schedule writes its input";
+  return "";
+}
+
+// The ranks a result expression folds, innermost first: a left fold over leaves, each of them
+// leaf(q, want) of input-chunk index `want` (cin chunks per rank), every rank once.
+static std::string foldRanks(const Exprs& ex, int e, int want, int cin, int n, std::vector<int>* ranks) {
+  std::vector<int> ord;  // leaf keys, outermost fold first
+  if (e < 0) return "a result chunk is not a fold of the inputs";
+  while (ex.at(e).a >= 0) {
+    const Expr& x = ex.at(e);
+    const bool la = ex.at(x.a).a < 0, lb = ex.at(x.b).a < 0;
+    if (la && lb) {
+      // the innermost fn(x_p, x_q): commutative, so the fold may start with either
+      int p = ex.at(x.a).b, q = ex.at(x.b).b;
+      if (p > q) std::swap(p, q);
+      ord.push_back(q);
+      ord.push_back(p);
+      e = -1;
+      break;
+    }
+    if (!la && !lb) return "a result chunk folds partial results in a tree shape";
+    ord.push_back(la ? ex.at(x.a).b : ex.at(x.b).b);
+    e = la ? x.b : x.a;
+  }
+  if (e >= 0) ord.push_back(ex.at(e).b);  // a lone leaf (no fold)
+  ranks->clear();
+  std::vector<bool> seen(n, false);
+  for (auto it = ord.rbegin(); it != ord.rend(); ++it) {
+    const int q = *it / cin, cc = *it % cin;
+    if (cc != want || seen[q]) return "a result chunk is not a fold of every rank's same chunk";
+    seen[q] = true;
+    ranks->push_back(q);
+  }
+  if ((int)ranks->size() != n) return "a result chunk misses a rank";
+  return "";
+}
+
+// classes of chunks whose orders (per rank) agree: ordOf[c][r] -> chunkClass, order
+static void classesOf(const std::vector<std::vector<std::vector<int>>>& ordOf, std::vector<int>* chunkClass,
+                      std::vector<std::vector<std::vector<int>>>* order) {
+  chunkClass->assign(ordOf.size(), -1);
+  order->clear();
+  for (size_t c = 0; c < ordOf.size(); c++) {
+    for (size_t k = 0; k < order->size() && (*chunkClass)[c] < 0; k++)
+      if ((*order)[k] == ordOf[c]) (*chunkClass)[c] = (int)k;
+    if ((*chunkClass)[c] < 0) {
+      (*chunkClass)[c] = (int)order->size();
+      order->push_back(ordOf[c]);
+    }
+  }
+}
+
+FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
+  FoldLowering out;
+  const int n = (int)byRank.size();
+  auto fail = [&](const std::string& why) {
+    out.ok = false;
+    out.why = why;
+    out.order.clear();
+    out.chunkClass.clear();
+    return out;
+  };
+  if (n < 2 || n > kMaxReduceFusion) return fail("ranks outside 2..16");
+  const Algorithm& a0 = byRank[0];
+  const int C = a0.nchunksPerLoop;
+  if (C <= 0) return fail("no chunks");
+  for (const Algorithm& a : byRank) {
+    if (!a.valid || a.coll != kAllReduce) return fail("not a valid AllReduce schedule");
+    if (a.proto != kProtoLL) return fail("protocol is not LL");
+    if (a.nchunksPerLoop != C || a.inPlace != a0.inPlace) return fail("ranks disagree on the loop shape");
+  }
+  Exprs ex;
+  std::vector<std::vector<int>> inB, outB;
+  const std::string why = symRun(byRank, C, C, false, ex, inB, outB);
+  if (!why.empty()) return fail(why);
   // every result chunk: a left fold of all ranks' same chunk; orders per (chunk, rank)
   std::vector<std::vector<std::vector<int>>> ordOf(C, std::vector<std::vector<int>>(n));
   for (int r = 0; r < n; r++) {
     const std::vector<int>& res = byRank[r].inPlace ? inB[r] : outB[r];
-    if (!byRank[r].inPlace)
-      for (int c = 0; c < C; c++)
-        if (inB[r][c] != ex.leaf(r, c, C)) return fail("an out-of-place schedule writes its input");
     for (int c = 0; c < C; c++) {
-      std::vector<int> ord;  // ranks, outermost fold last
-      int e = res[c];
-      if (e < 0) return fail("a result chunk is not a fold of the inputs");
-      while (ex.at(e).a >= 0) {
-        const Expr& x = ex.at(e);
-        const bool la = ex.at(x.a).a < 0, lb = ex.at(x.b).a < 0;
-        if (la && lb) {
-          // the innermost fn(x_p, x_q): commutative, so the fold may start with either
-          int p = ex.at(x.a).b, q = ex.at(x.b).b;
-          if (p > q) std::swap(p, q);
-          ord.push_back(q);
-          ord.push_back(p);
-          e = -1;
-          break;
-        }
-        if (!la && !lb) return fail("a result chunk folds partial results in a tree shape");
-        ord.push_back(la ? ex.at(x.a).b : ex.at(x.b).b);
-        e = la ? x.b : x.a;
-      }
-      if (e >= 0) ord.push_back(ex.at(e).b);  // a lone leaf (no fold)
-      std::vector<int> ranks;
-      std::vector<bool> seen(n, false);
-      for (auto it = ord.rbegin(); it != ord.rend(); ++it) {
-        const int q = *it / C, cc = *it % C;
-        if (cc != c || seen[q]) return fail("a result chunk is not a fold of every rank's same chunk");
-        seen[q] = true;
-        ranks.push_back(q);
-      }
-      if ((int)ranks.size() != n) return fail("a result chunk misses a rank");
-      ordOf[c][r] = ranks;
+      const std::string w = foldRanks(ex, res[c], c, C, n, &ordOf[c][r]);
+      if (!w.empty()) return fail(w);
     }
   }
-  // classes: chunks whose orders agree on every rank
-  out.chunkClass.assign(C, -1);
-  for (int c = 0; c < C; c++) {
-    for (size_t k = 0; k < out.order.size() && out.chunkClass[c] < 0; k++)
-      if (out.order[k] == ordOf[c]) out.chunkClass[c] = (int)k;
-    if (out.chunkClass[c] < 0) {
-      out.chunkClass[c] = (int)out.order.size();
-      out.order.push_back(ordOf[c]);
-    }
-  }
+  classesOf(ordOf, &out.chunkClass, &out.order);
   if ((int)out.order.size() > kMaxFoldClasses) return fail("more fold orders than the fold kernel holds");
   if (out.order.size() > 1 && C > kMaxFoldChunks) return fail("more chunks than the fold kernel's class map holds");
   out.ok = true;
   // the two-phase form: every rank's chunk c is the same value (hash-consed: the same node), and
   // its creator owns it; every rank must own C / n chunks (the kernel deals the owned chunks of all
   // ranks out to its workgroups in lockstep)
-  auto notTwoPhase = [&](const std::string& why) {
+  auto notTwoPhase = [&](const std::string& w) {
     out.twoPhase = false;
-    out.whyNotTwoPhase = why;
+    out.whyNotTwoPhase = w;
     out.owner.clear();
     return out;
   };
@@ -312,6 +347,63 @@ FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank) {
   for (int q = 0; q < n; q++)
     if (owned[q] != C / n) return notTwoPhase("ranks own different numbers of chunks");
   out.twoPhase = true;
+  return out;
+}
+
+DirectLowering analyzeDirectLowering(const std::vector<Algorithm>& byRank) {
+  DirectLowering out;
+  const int n = (int)byRank.size();
+  auto fail = [&](const std::string& why) {
+    out = DirectLowering();
+    out.why = why;
+    return out;
+  };
+  if (n < 2 || n > kMaxReduceFusion) return fail("ranks outside 2..16");
+  const Algorithm& a0 = byRank[0];
+  const int C = a0.nchunksPerLoop;
+  if (C <= 0 || C % n != 0) return fail("no chunks, or chunks that do not divide over the ranks");
+  const int coll = a0.coll;
+  if (coll != kAllReduce && coll != kReduceScatter && coll != kAllGather)
+    return fail("not an AllReduce, ReduceScatter or AllGather");
+  for (const Algorithm& a : byRank) {
+    if (!a.valid || a.coll != coll) return fail("ranks disagree on the collective");
+    if (a.proto != kProtoSimple) return fail("protocol is not Simple");
+    if (a.nchunksPerLoop != C || a.inPlace != a0.inPlace) return fail("ranks disagree on the loop shape");
+    if (coll != kAllReduce && a.inPlace) return fail("an in-place ReduceScatter / AllGather schedule");
+  }
+  // chunks per rank buffer: the AllGather's input is one rank's block, the ReduceScatter's output
+  const int cin = coll == kAllGather ? C / n : C, cout = coll == kReduceScatter ? C / n : C;
+  Exprs ex;
+  std::vector<std::vector<int>> inB, outB;
+  const std::string why = symRun(byRank, cin, cout, true, ex, inB, outB);
+  if (!why.empty()) return fail(why);
+  out.coll = coll;
+  if (coll == kAllGather) {
+    // the AllGather's definition: output chunk c of every rank is rank c / (C / n)'s input chunk
+    for (int r = 0; r < n; r++)
+      for (int c = 0; c < C; c++)
+        if (outB[r][c] != ex.leaf(c / cin, c % cin, cin)) return fail("an output chunk is not its rank's input chunk");
+    out.ok = true;
+    return out;
+  }
+  // ReduceScatter: rank r's output chunk c folds every rank's input chunk r * C / n + c; AllReduce:
+  // every rank's chunk c folds every rank's chunk c, and every rank holds the same value (one rank
+  // computes it for all: the direct kernel's owner)
+  std::vector<std::vector<std::vector<int>>> ordOf(cout, std::vector<std::vector<int>>(n));
+  for (int r = 0; r < n; r++) {
+    const std::vector<int>& res = byRank[r].inPlace ? inB[r] : outB[r];
+    for (int c = 0; c < cout; c++) {
+      const int want = coll == kReduceScatter ? r * cout + c : c;
+      const std::string w = foldRanks(ex, res[c], want, cin, n, &ordOf[c][r]);
+      if (!w.empty()) return fail(w);
+      if (coll == kAllReduce && res[c] != (byRank[0].inPlace ? inB[0][c] : outB[0][c]))
+        return fail("ranks hold different folds of a chunk");
+    }
+  }
+  classesOf(ordOf, &out.chunkClass, &out.order);
+  if ((int)out.order.size() > kMaxDirectClasses) return fail("more fold orders than the direct kernel holds");
+  if (cout > kMaxFoldChunks) return fail("more chunks than the direct kernel's class map holds");
+  out.ok = true;
   return out;
 }
 
@@ -352,6 +444,36 @@ FoldLowering lowerScheduleFile(const std::string& path, int nRanks) {
   if (cache.size() > 256) cache.clear();  // a bound for long-lived processes
   cache.emplace(key, fl);
   return fl;
+}
+
+DirectLowering directScheduleFile(const std::string& path, int nRanks) {
+  std::string text;
+  if (FILE* f = fopen(path.c_str(), "rb")) {
+    char buf[65536];
+    size_t got;
+    while ((got = fread(buf, 1, sizeof(buf), f)) > 0) text.append(buf, got);
+    fclose(f);
+  }
+  static std::mutex mu;
+  static std::map<std::pair<std::string, int>, DirectLowering> cache;
+  const auto key = std::make_pair(text, nRanks);
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  DirectLowering dl;
+  std::vector<Algorithm> byRank(nRanks);
+  for (int r = 0; r < nRanks; r++)
+    if (loadAlgoFromXml(path.c_str(), &byRank[r], kMaxChannels, r, nRanks) != 0) {
+      dl.why = "the schedule does not load for rank " + std::to_string(r);
+      return dl;
+    }
+  dl = analyzeDirectLowering(byRank);
+  std::lock_guard<std::mutex> g(mu);
+  if (cache.size() > 256) cache.clear();
+  cache.emplace(key, dl);
+  return dl;
 }
 
 }  // namespace msccl

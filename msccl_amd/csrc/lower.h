@@ -33,6 +33,31 @@ struct FoldLowering {
   std::vector<int> owner;
 };
 FoldLowering analyzeFoldLowering(const std::vector<Algorithm>& byRank);
+
+// The direct form of a Simple schedule (the reference's P2P direct mode, prims_simple.h:75-128,
+// 500-560: within one process a sender writes straight into the receiver's buffer).  When every
+// rank of a communicator sits in one fused launch (ncclCommInitAll on one GPU, one group call),
+// every rank's buffers are addressable from the launch and ready at its start, so the schedule's
+// values need no FIFO at all:
+//   AllGather (out of place): ok when every output chunk is its rank's input chunk (the
+//     AllGather's definition): each rank writes its input into every rank's output once;
+//   ReduceScatter (out of place): ok when rank r's output chunk c is a left fold of every rank's
+//     input chunk r C / n + c; rank r reads every rank's block and folds it in order[k][r];
+//   AllReduce: ok when chunk c is one left fold of every rank's chunk c, the same value on every
+//     rank; rank r folds its share of the packs in order[k][.] and writes it to every rank.
+// Simple's semantics: `re` folds (s_0 (+) s_1 ...) (+) d (prims_simple.h:258-263; calls whose every
+// transfer moves at least nthreads elements, plan.cc: the direct plan's guard), rrs / rrc
+// fn(local, peer).  chunkClass is per output chunk (RS: C / n of them).
+struct DirectLowering {
+  bool ok = false;
+  std::string why;
+  int coll = -1;
+  std::vector<int> chunkClass;
+  std::vector<std::vector<std::vector<int>>> order;
+};
+DirectLowering analyzeDirectLowering(const std::vector<Algorithm>& byRank);
+// the file loaded for each of nRanks ranks, then analyzeDirectLowering (cached like lowerScheduleFile)
+DirectLowering directScheduleFile(const std::string& path, int nRanks);
 // The schedule file at `path` loaded for each of nRanks ranks, then analyzeFoldLowering; cached
 // per process by (file text, nRanks), so the co-resident communicators of one process (each
 // rank loads it for every rank) parse and analyse a file once.  A file that does not load for

@@ -88,6 +88,7 @@ Knobs Knobs::fromEnv() {
   k.lowerLarge = envInt("MSCCL_AMD_LOWER_LARGE", 1) != 0;
   k.forceRemote = envInt("MSCCL_AMD_FORCE_REMOTE", 0) != 0;
   k.twoPhaseStep = (int32_t)envInt("MSCCL_AMD_TWO_PHASE_STEP", 0);
+  k.direct = envInt("MSCCL_AMD_DIRECT", 1) != 0;
   return k;
 }
 
@@ -432,6 +433,27 @@ int makeRingPlan(const CallDesc& c, const Knobs& k, Plan* p) {
   return 0;
 }
 
+// The direct form (lower.h: DirectLowering) for this call of a Simple schedule: op Sum..Min, every
+// interpreter iteration moving at least nthreads elements per chunk (there Simple's `re` folds
+// (s_0 (+) ...) (+) d, the order the analysis read; below it the reference takes the per-element
+// d-first path, msccl_interpreter.h:157-170), and with several fold orders output chunks of whole
+// 16-B packs (each pack folds in its chunk's order).  Sets p->directOk; the launch decides
+// (enqueue.cc: launchGroup: every rank of the communicator in it).
+static void directEligible(const CallDesc& c, const Knobs& k, int classes, Plan* p) {
+  p->directOk = false;
+  if (!k.direct || p->proto != kProtoSimple || c.redop > kDevMin || p->nBytes > (1ll << 30)) return;
+  const int64_t sp = p->sizePerChunk, cs = p->chunkSize;
+  if (c.coll != kAllGather) {
+    if (sp < p->refNthreads) return;
+    const int64_t tail = cs > 0 ? sp % cs : 0;
+    if (tail != 0 && tail < p->refNthreads) return;
+  }
+  const int64_t pe = 16 / refTypeSize(p->dtype);
+  if (classes > 1 && (sp % pe != 0 || sp / pe > INT32_MAX)) return;
+  p->directChunkPacks = classes > 1 ? sp / pe : 0;
+  p->directOk = true;
+}
+
 int planCall(const PlanContext& ctx, const CallDesc& c, bool asyncMany, Plan* p) {
   const std::vector<Algorithm>& algos = *ctx.algos;
   const Knobs& k = *ctx.knobs;
@@ -477,6 +499,8 @@ int planCall(const PlanContext& ctx, const CallDesc& c, bool asyncMany, Plan* p)
   }
   const int r = makePlan(algos, idx, protoOverride, c, k, p);
   if (r != 0) return r;
+  const int dcls = ctx.directClasses && (size_t)idx < ctx.directClasses->size() ? (*ctx.directClasses)[idx] : 0;
+  if (dcls > 0 && ctx.oneLaunch) directEligible(c, k, dcls, p);
   const int classes = ctx.foldClasses && (size_t)idx < ctx.foldClasses->size() ? (*ctx.foldClasses)[idx] : 0;
   const bool twoPhase = ctx.foldTwoPhase && (size_t)idx < ctx.foldTwoPhase->size() && (*ctx.foldTwoPhase)[idx];
   if (classes > 0 && ctx.flat && lowerToFoldPlan(c, k, classes, twoPhase, p) == 0) {

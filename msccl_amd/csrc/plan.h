@@ -55,6 +55,11 @@ struct Plan {
   // a lowered schedule's kernel (lowerToFoldPlan): kLowerFold, or for calls above the fold's
   // limit kLowerPair (2 ranks) / kLowerTwoPhase
   int lowerMode = 0;
+  // the call may run the schedule's direct form (planCall: directEligible) if every rank of the
+  // communicator is in its launch (enqueue.cc: launchGroup decides); the plan is otherwise the
+  // schedule's own.  directChunkPacks: 16-B packs per output chunk for the class lookup (0: one class)
+  bool directOk = false;
+  int64_t directChunkPacks = 0;
 };
 enum : int { kLowerFold = 0, kLowerPair = 1, kLowerTwoPhase = 2 };
 // 16-B packs per FIFO step of the two-phase fold (a slot holds 2048 at the default LL FIFO)
@@ -92,6 +97,7 @@ struct Knobs {
                              // (2 ranks: the pair kernel; more: the two-phase fold; plan.cc: lowerLargePlan)
   int32_t forceRemote;       // MSCCL_AMD_FORCE_REMOTE: every peer treated as on another GPU (a test knob)
   int32_t twoPhaseStep;      // MSCCL_AMD_TWO_PHASE_STEP: 16-B packs per FIFO step of the two-phase fold (0: default)
+  int32_t direct;            // MSCCL_AMD_DIRECT: Simple schedules' direct form when every rank is in one launch
   static Knobs fromEnv();
 };
 
@@ -168,6 +174,8 @@ struct PlanContext {
   const Knobs* knobs = nullptr;                   // after init's agreed adjustments (FIFO sizes)
   const std::vector<int>* foldClasses = nullptr;  // per algorithm: fold orders when lowered, else 0
   const std::vector<int>* foldTwoPhase = nullptr; // per algorithm: the lowering has a two-phase form
+  const std::vector<int>* directClasses = nullptr; // per algorithm: the direct form's fold orders, 0: none
+  bool oneLaunch = false;     // the communicator's group calls are one fused launch (ncclComm::clique)
   bool flat = false;          // the flat group's connections exist (transport.cc: flatEnabled)
   bool ringFallback = true;   // MSCCL_AMD_RING_FALLBACK
   size_t scratchSize = 0;     // MSCCL scratch allocated at init

@@ -692,6 +692,34 @@ ncclResult_t algoUpload(ncclComm* comm) {
     comm->algoPair[g] = exchangeOnly && g < comm->algoFuse.size() ? pairFormOf(a, comm->algoFuse[g]) : ncclComm::PairForm();
     NCCLCHECK(uploadImages(img, &d));
   }
+  // the direct forms' programs (interpreter.h: DirectRunner): transfer 0 lists this rank's fold
+  // order (ranks) per class (srcoff = classes), transfer 1 every output chunk's class (srcoff =
+  // chunks); the AllGather needs none
+  comm->directAlgos.assign(comm->algos.size(), DevAlgoHost());
+  for (size_t g = 0; g < comm->algoDirect.size() && g < comm->algos.size(); g++) {
+    const ncclComm::DirectProgram& dp = comm->algoDirect[g];
+    if (dp.coll < 0 || dp.coll == kAllGather) continue;
+    std::vector<int16_t> reds;
+    std::vector<Transfer> ts(2);
+    ts[0].srcoff = (int16_t)dp.order.size();
+    ts[0].redPtr = 0;
+    for (const std::vector<int>& o : dp.order)
+      for (int q : o) reds.push_back((int16_t)q);
+    ts[1].srcoff = (int16_t)dp.chunkClass.size();
+    ts[1].redPtr = (int16_t)reds.size();
+    for (int k : dp.chunkClass) reds.push_back((int16_t)k);
+    DevAlgoHost& d = comm->directAlgos[g];
+    d.nBlocks = 1;
+    d.tbStride = (int)imageBytes(ts.size(), 0, reds.size());  // read from global memory (DirectShared tables)
+    std::vector<char> img((size_t)d.tbStride, 0);
+    DevTbHeader h;
+    memset(&h, 0, sizeof(h));
+    h.nsteps = (uint16_t)ts.size();
+    h.nreds = (uint16_t)reds.size();
+    const std::vector<int16_t> none;
+    putImage(img, 0, h, ts, none, none, reds);
+    NCCLCHECK(uploadImages(img, &d));
+  }
   return ringUpload(comm);
 }
 

@@ -16,7 +16,8 @@ STUB = r"""
 #include "device/devcomm.h"
 namespace msccl {
 #define STUB(N, STAMP) LaunchFn N[6][3] = {}; LaunchFn N##_small[2][4] = {}; LaunchFn N##_fold[4] = {}; \
-  LaunchFn N##_pair[4] = {}; LaunchFn N##_two[4] = {}; OneRankFn N##_one = nullptr;                \
+  LaunchFn N##_pair[4] = {}; LaunchFn N##_two[4] = {}; LaunchFn N##_direct[4] = {};                \
+  OneRankFn N##_one = nullptr;                                                                     \
   extern const uint32_t N##_layout = STAMP;
 STUB(gLaunch_i8, kWorkLayout) STUB(gLaunch_u8, kWorkLayout) STUB(gLaunch_i32, kWorkLayout)
 STUB(gLaunch_u32, kWorkLayout) STUB(gLaunch_i64, kWorkLayout) STUB(gLaunch_u64, kWorkLayout)
@@ -31,7 +32,8 @@ def _build(tmp_path, bad_f32, bad_bf16):
     src = tmp_path / "stub.cc"
     src.write_text(STUB)
     out = tmp_path / ("stub_%d_%d.so" % (bad_f32, bad_bf16))
-    cmd = ["g++", "-std=c++17", "-shared", "-fPIC", "-O1", "-I", os.path.join(ROOT, "msccl_amd", "csrc"),
+    # -Bsymbolic: the stub's own stamps, not those of a libmsccl_amd.so the process loaded globally
+    cmd = ["g++", "-std=c++17", "-shared", "-fPIC", "-O1", "-Wl,-Bsymbolic", "-I", os.path.join(ROOT, "msccl_amd", "csrc"),
            "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
            "-DBAD_F32=%d" % bad_f32, "-DBAD_BF16=%d" % bad_bf16, str(src),
            os.path.join(ROOT, "msccl_amd", "csrc", "device", "dispatch.cc"), "-o", str(out)]
