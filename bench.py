@@ -62,6 +62,8 @@ def parse(argv=None):
     ap.add_argument("--pmc", default="auto", choices=("auto", "off"),
                     help="auto: at N=1 measure the headline launch's HBM traffic with two rocprofv3 PMC "
                          "passes (FETCH_SIZE, WRITE_SIZE) of a headline-only child run")
+    ap.add_argument("--no-tuning", action="store_true",
+                    help="at --gpus N > 1 skip the tuning keys (run_tuning: lowering caps, Simple FIFO sizes, link rate)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -185,14 +187,16 @@ def lowered_bytes(last: dict, n: int, nbytes: int):
     return None
 
 
+PAIR_TIERS = "0:4096:1:p,4096:1073741825:16:p"   # the 2-rank pair one-shot tiers of rounds 2-5
+
+
 def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None, remote: bool = False):
     """All-pairs schedules in size tiers, as a user registers several msccl-tools XMLs with
     minBytes/maxBytes (MSCCL_XML_FILES, at most 4): [(lo, hi, instances, path, kind)].  At 2
-    ranks the one-shot all-pairs form (xmlgen.allreduce_oneshot; both ranks get identical bits
-    for n = 2) serves sizes below 16 MiB and the two-phase all-pairs the rest; the large tier uses
-    inst_large.  At more ranks: rank-ordered one-shot (4 instances; lowered to the one-hop fold)
-    below 64 KiB, then two-phase all-pairs with 4 instances below 4 MiB and inst_large above.
-    remote (one rank per GPU, peers over xGMI): inst_large from 64 KiB on."""
+    ranks the two-phase all-pairs, one instance below 4 KiB and inst_large above.  At more ranks:
+    rank-ordered one-shot (4 instances; lowered to the one-hop fold) below 64 KiB, then two-phase
+    all-pairs with 4 instances below 4 MiB and inst_large above.  remote (one rank per GPU, peers
+    over xGMI): inst_large from 64 KiB on."""
     if tiers_arg:
         # lo:hi:instances[:kind], kind "a" = two-phase all-pairs (default), "o" = one-shot,
         # "O" = rank-ordered one-shot, "p" = 2-rank one-hop exchange (s, rrc), "r" = ring with
@@ -202,13 +206,14 @@ def make_xmls(n: int, proto: str, inst_large: int, tmp: str, tiers_arg=None, rem
             f = t.split(":")
             spec.append((int(f[0]), int(f[1]), int(f[2])) + ((f[3],) if len(f) > 3 else ()))
     elif n <= 2:
-        # Two ranks: the all-pairs exchange fused into one hop per thread block (s, rrc:
-        # xmlgen.allreduce_pair_oneshot): no scratch, no cross-tb dependency, 7 S HBM bytes per
-        # rank against the two-phase schedule's 7.5 S.  One instance below 4 KiB (latency), 16
-        # above; measured over the whole sweep against the two-phase all-pairs and ring forms
-        # (profiles/r02_tier_sweep2.txt): 128 B 14.8 -> 11.8 us, 1 MiB 50 -> 78 GB/s,
-        # 32 MiB 398 -> 450 GB/s
-        spec = [(0, 4 << 10, 1, "p"), (4 << 10, (1 << 30) + 1, inst_large, "p")]
+        # Two ranks: the msccl-tools two-phase all-pairs XML itself (the north star's schedule),
+        # one instance below 4 KiB, inst_large above.  The runtime lowers it at upload
+        # (msccl_amd/csrc/lower.cc): calls up to 4 KiB run the one-hop fold, larger ones the pair
+        # exchange on the flat connections (6 S HBM bytes per rank against the schedule's 7.5 S),
+        # with the schedule's values.  Same box, driver form (--steps 20), against the pair
+        # one-shot XML (PAIR_TIERS, rounds 2-5): 32 MiB 535.4 -> 546.8 GB/s, sweep average
+        # 116.4 -> 120.8 (profiles/r06g_c2_pair.json, r06g_c2_allpairs.json)
+        spec = [(0, 4 << 10, 1, "a"), (4 << 10, (1 << 30) + 1, inst_large, "a")]
     else:
         # rank-ordered one-shot (s, r, re, cpy; the same bits on every rank) below 64 KiB: the
         # runtime lowers it to the one-hop fold there (msccl_amd/csrc/lower.cc), which beats the
@@ -288,19 +293,25 @@ def config_id(n: int, proto: str, dtname: str) -> str:
     return ""
 
 
-def workload_desc(multi: bool, n: int, proto: str, dtname: str, one_gpu: bool = False) -> str:
+SCHEDULE_NAMES = {"a": "msccl-tools two-phase all-pairs XML", "o": "one-shot all-pairs XML",
+                  "O": "rank-ordered one-shot all-pairs XML", "p": "pair one-shot XML (s, rrc; not all-pairs)",
+                  "r": "ring XML"}
+
+
+def workload_desc(multi: bool, n: int, proto: str, dtname: str, one_gpu: bool = False, kind: str = "a") -> str:
+    """The workload label: the config, the schedule the headline size actually ran (kind: its
+    tier's, make_xmls), the placement."""
     cid = config_id(n, proto, dtname)
+    sched = SCHEDULE_NAMES[kind]
     if not multi:
-        return ("%s%d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
-                "(fused launch, local HBM in place of xGMI)" % (cid + " shape: " if cid else "", n, proto, dtname)
-                if cid != "C2" else
-                "C2: %d-rank all-pairs %s AllReduce, %s, ranks co-resident on one MI355X "
-                "(fused launch, local HBM in place of xGMI)" % (n, proto, dtname))
+        return ("%s%d-rank %s AllReduce through the %s, %s, ranks co-resident on one MI355X "
+                "(fused launch, local HBM in place of xGMI)"
+                % ((cid + ": ") if cid == "C2" else (cid + " shape: ") if cid else "", n, proto, sched, dtname))
     if one_gpu:
         return ("rehearsal: %d rank processes sharing one MI355X (hipIpc FIFOs, local HBM in place of "
-                "xGMI), all-pairs %s AllReduce, %s" % (n, proto, dtname))
-    return ("%s: %d-rank all-pairs %s AllReduce over xGMI, %s, one rank per GPU"
-            % (cid or "%d-GPU" % n, n, proto, dtname))
+                "xGMI), %s AllReduce through the %s, %s" % (n, proto, sched, dtname))
+    return ("%s: %d-rank %s AllReduce through the %s over xGMI, %s, one rank per GPU"
+            % (cid or "%d-GPU" % n, n, proto, sched, dtname))
 
 
 TIER_KINDS = {"a": "allreduce_allpairs (two-phase: s, r, re, s, r; msccl-tools form)",
@@ -325,6 +336,23 @@ def pmc_traffic(cfg_key: dict, src_hash: str):
         if all(c.get(k, {} if k == "knobs" else None) == v for k, v in cfg_key.items()) and pmc.get("traffic_bytes_per_launch"):
             return round(pmc["traffic_bytes_per_launch"]), os.path.relpath(f, ROOT)
     return None, None
+
+
+_STREAMS = {}
+
+
+def bench_stream(dev):
+    """One collective stream per device for the whole run: every part of the bench launches on it.
+    A stream is a hardware queue; rank processes that share one GPU (the one-GPU rehearsal) and
+    each hold several would oversubscribe the GPU's queues, which the command processor then
+    time-slices (about 11 ms per slice, profiles/r06h_rehearse_8.json)."""
+    import torch
+    key = str(dev)
+    if key not in _STREAMS:
+        _STREAMS[key] = torch.cuda.Stream(dev)
+    s = _STREAMS[key]
+    s.wait_stream(torch.cuda.current_stream(dev))
+    return s
 
 
 def init_comms(multi: bool, world: int, rank: int, n: int):
@@ -389,7 +417,7 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
     comms = init_comms(multi, world, rank, n)
     note("init done")
     ts = M.TYPE_SIZE[dt]
-    stream = torch.cuda.Stream(dev)
+    stream = bench_stream(dev)
     nloc = len(comms)
     try:
         ranks = [rank] if multi else list(range(n))
@@ -509,6 +537,118 @@ def run_extra(cfg: str, a, multi: bool, world: int, rank: int, n: int, tmp: str)
             c.destroy()
 
 
+TUNE_SIZES = (64 << 10, 128 << 10, 256 << 10, 512 << 10, 1 << 20)
+TUNE_LOWER_CAPS = (128 << 10, 256 << 10, 512 << 10)
+TUNE_BUFFSIZES = (256 << 10, 4 << 20)
+
+
+def run_tuning(a, world: int, rank: int, n: int, tmp: str, dt: int, headline_xmls: str, sweep, xgmi_cal,
+               one_gpu: bool) -> dict:
+    """bench.py --gpus N (N > 1, one rank per process): the data that sets the defaults tuned on
+    co-resident ranks for one rank per GPU, in bounded extra keys of the line:
+      lower_max_bytes  the headline's schedules at 64 KiB - 1 MiB with MSCCL_AMD_LOWER_MAX_BYTES
+                       = 128 / 256 / 512 KiB and with the default (plan.h: defaultLowerMaxBytes,
+                       the link model's crossover): where the lowered one-hop fold stops paying;
+      buffsize         (N = 8) C4 / C5 with NCCL_BUFFSIZE = 256 KiB / 4 MiB (the Simple FIFO,
+                       4 MiB by default towards other GPUs);
+      link             the one-way cuda:0 -> cuda:1 copy rate and the 128 B AllReduce time (an
+                       upper bound of the hop latency L the §8b model assumes to be 2 us).
+    Every size is timed like the sweep (K steps in one hipGraph, barrier + max over ranks) and
+    checked once on exact integers; C4 / C5 as the configs key times them."""
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ts = M.TYPE_SIZE[dt]
+    tdt = {M.FLOAT32: torch.float32, M.FLOAT16: torch.float16, M.BFLOAT16: torch.bfloat16}[dt]
+    k = max(1, min(a.steps, 20))
+    out = {"steps": k, "lower_max_bytes": {}}
+    buf = torch.empty(max(TUNE_SIZES) // ts, dtype=tdt, device=dev).uniform_(-1, 1)
+    stream = bench_stream(dev)
+    stream.wait_stream(torch.cuda.current_stream(dev))
+
+    def maxed(vals):
+        tt = torch.tensor(vals, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        return [float(v) for v in tt]
+
+    saved = {v: os.environ.get(v) for v in ("MSCCL_AMD_LOWER_MAX_BYTES", "NCCL_BUFFSIZE", "MSCCL_XML_FILES")}
+    try:
+        os.environ["MSCCL_XML_FILES"] = headline_xmls
+        for cap in (None,) + TUNE_LOWER_CAPS:
+            if cap is None:
+                os.environ.pop("MSCCL_AMD_LOWER_MAX_BYTES", None)
+            else:
+                os.environ["MSCCL_AMD_LOWER_MAX_BYTES"] = str(cap)
+            comm = init_comms(True, world, rank, n)[0]
+            rows = {}
+            try:
+                for nbytes in TUNE_SIZES:
+                    cnt = nbytes // ts
+
+                    def step():
+                        comm.all_reduce(buf.data_ptr(), buf.data_ptr(), cnt, dt, M.SUM, stream.cuda_stream)
+                    for _ in range(max(1, a.warmup)):
+                        step()
+                    # the sweep's timing: the K steps captured into one hipGraph, replayed once
+                    # untimed, then timed (a rank's launches do not wait on its host)
+                    torch.cuda.synchronize()
+                    graph = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(graph, stream=stream, capture_error_mode="relaxed"):
+                        for _ in range(k):
+                            step()
+                    with torch.cuda.stream(stream):
+                        graph.replay()
+                    torch.cuda.synchronize()
+                    torch.distributed.barrier()
+                    t0 = time.perf_counter()
+                    with torch.cuda.stream(stream):
+                        graph.replay()
+                    torch.cuda.synchronize()
+                    torch.distributed.barrier()
+                    t = maxed([(time.perf_counter() - t0) / k])[0]
+                    del graph
+                    if comm.async_error() != 0:
+                        raise RuntimeError("kernel reported an error at %d bytes" % nbytes)
+                    last = comm.info()["last"]
+                    j = torch.arange(cnt, device=dev, dtype=torch.int64)
+                    buf[:cnt].copy_((((j * 7 + rank * 3 + (j >> 5)) % 9) - 4).to(tdt))
+                    want = sum((((j * 7 + r * 3 + (j >> 5)) % 9) - 4).float() for r in range(n)).to(tdt)
+                    torch.cuda.synchronize()
+                    step()
+                    torch.cuda.synchronize()
+                    good = maxed([0.0 if torch.equal(buf[:cnt], want) else 1.0])[0] == 0.0
+                    rows[str(nbytes)] = {"us": round(t * 1e6, 2), "kernel": kernel_name(last), "verified": good}
+            finally:
+                comm.destroy()
+            out["lower_max_bytes"]["default" if cap is None else str(cap)] = rows
+        os.environ.pop("MSCCL_AMD_LOWER_MAX_BYTES", None)
+        if world == 8:
+            out["buffsize"] = {}
+            for bs in TUNE_BUFFSIZES:
+                os.environ["NCCL_BUFFSIZE"] = str(bs)
+                row = {}
+                for cfg in ("C4", "C5"):
+                    try:
+                        r = run_extra(cfg, a, True, world, rank, n, tmp)
+                        row[cfg] = {p: r[p]["kernel_ms"] for p in ("allreduce", "reduce_scatter", "all_gather") if p in r}
+                        row[cfg]["verified"] = r["verified"]
+                    except Exception as e:  # noqa: BLE001  (reported, the headline stands)
+                        row[cfg] = {"error": str(e)[:200]}
+                out["buffsize"][str(bs)] = row
+    finally:
+        for v, x in saved.items():
+            if x is None:
+                os.environ.pop(v, None)
+            else:
+                os.environ[v] = x
+    out["link"] = {"copy_gbs_0_to_1": xgmi_cal,
+                   "copy_note": None if xgmi_cal is not None else
+                   ("ranks share one GPU (rehearsal): no link to measure" if one_gpu else "peer copy failed"),
+                   "allreduce_%dB_us" % sweep[0]["bytes"]: round(sweep[0]["ms"] * 1e3, 2)}
+    out["verified"] = all(r["verified"] for rows in out["lower_max_bytes"].values() for r in rows.values()) and \
+        all(c.get("verified", False) for row in out.get("buffsize", {}).values() for c in row.values())
+    return out
+
+
 RCCL_32TB = "/opt/rocm/share/rccl/msccl-algorithms/allreduce-allpairs-8n-ll-32tb.xml"
 
 
@@ -518,9 +658,15 @@ def secondary_schedules(multi: bool, n: int, nbytes: int):
     the shape of the RCCL-shipped allreduce-allpairs-8n XMLs) at the headline's ranks and size, and
     (2) at N=1 the RCCL-shipped 8n-32tb LL schedule itself on 8 co-resident ranks, fp16 (config C3's
     shape; maxBytes raised from 64 KiB so it admits 32 MiB, as tests/test_gpu_configs.py does).
+    At 2 ranks the headline already runs the two-phase all-pairs XML: the line beside it is the
+    pair one-shot XML (xmlgen.allreduce_pair_oneshot x16, the headline schedule of rounds 2-5).
     Returns [(name, xml_text, ranks, bytes, dtype)]."""
-    out = [("allpairs_two_phase", xmlgen.allreduce_allpairs(n, 16 if n <= 2 else 4, "LL", True, 0, 1 << 40,
-                                                             name="sec_allpairs"), n, nbytes, None)]
+    if n <= 2:
+        out = [("pair_oneshot", xmlgen.allreduce_pair_oneshot(16, "LL", True, 0, 1 << 40, name="sec_pair"),
+                n, nbytes, None)]
+    else:
+        out = [("allpairs_two_phase", xmlgen.allreduce_allpairs(n, 4, "LL", True, 0, 1 << 40,
+                                                                 name="sec_allpairs"), n, nbytes, None)]
     if not multi and os.path.exists(RCCL_32TB):
         x = open(RCCL_32TB).read().replace('maxBytes="65536"', 'maxBytes="%d"' % ((32 << 20) + 1))
         out.append(("rccl_allpairs_8n_ll_32tb", x, 8, 32 << 20, M.FLOAT16))
@@ -545,7 +691,7 @@ def run_secondary(name: str, xml_text: str, n: int, nbytes: int, dt: int, a, mul
         tdt = {M.FLOAT32: torch.float32, M.FLOAT16: torch.float16, M.BFLOAT16: torch.bfloat16}[dt]
         ranks = [rank] if multi else list(range(n))
         bufs = [torch.empty(cnt, dtype=tdt, device=dev).uniform_(-1, 1) for _ in ranks]
-        stream = torch.cuda.Stream(dev)
+        stream = bench_stream(dev)
         stream.wait_stream(torch.cuda.current_stream(dev))
 
         def step():
@@ -744,7 +890,7 @@ def main():
         if rank == 0 and torch.cuda.device_count() > 1 and not one_gpu:
             xgmi_cal = calibrate_xgmi()
         barrier()
-    stream = torch.cuda.Stream(devs[0])
+    stream = bench_stream(devs[0])
     stream.wait_stream(torch.cuda.current_stream(devs[0]))
     maxb = max(sizes)
     bufs = [torch.empty(maxb // 4 + 64, dtype=torch.float32, device=d).uniform_(-1, 1) for d in devs]
@@ -901,10 +1047,11 @@ def main():
         roof["xgmi"] = {"busbw": head["busbw"], "peak": link, "frac": round(head["busbw"] / link, 4),
                         "ll_ceiling": round(link * {0: 0.5, 1: 0.75}.get(proto_id, 1.0), 1),
                         "link_gbs_assumed": XGMI_LINK_GBS, "link_gbs_measured": xgmi_cal}
-    workload = workload_desc(multi, n, a.proto, dtname, one_gpu)
+    workload = workload_desc(multi, n, a.proto, dtname, one_gpu, head["tier"])
     knobs = {k: v for k, v in sorted(os.environ.items()) if k.startswith("MSCCL_AMD_") and k != "MSCCL_AMD_TIMEOUT_SEC"}
     cfg_key = {"workload": workload, "bytes_per_rank": head["bytes"], "instances_large": inst, "knobs": knobs}
-    schedule = TIER_KINDS[head["tier"]] + (", s + rrc fused into one pass" if head["fused"] else "")
+    schedule = TIER_KINDS[head["tier"]] + (", s + rrc fused into one pass" if head["fused"] else "") + \
+        (", lowered at upload: runs as %s (msccl_amd/csrc/lower.cc)" % head["kernel"] if head["lowered"] else "")
     e2e = None
     if a.e2e and rank == 0 and not multi:
         e2e = measure_e2e(comms, n, maxb, dt, ts, stream, devs[0])
@@ -944,6 +1091,12 @@ def main():
             extras[cfg] = run_extra(cfg, a, multi, world, rank, n, tmp)
         except Exception as e:  # noqa: BLE001  (reported in the JSON line, the headline stands)
             extras[cfg] = {"error": str(e)[:300]}
+    tuning = None
+    if multi and world > 1 and not a.no_tuning:
+        try:
+            tuning = run_tuning(a, world, rank, n, tmp, dt, ":".join(t[3] for t in tiers), results, xgmi_cal, one_gpu)
+        except Exception as e:  # noqa: BLE001  (reported in the JSON line, the headline stands)
+            tuning = {"error": str(e)[:300]}
     cpu = None
     if not a.no_cpu and rank == 0 and not multi:   # the host baseline is quoted at N=1 only
         cpu = cpu_baseline(n, maxb, dt if dt in (6, 7, 9) else 7, a.cpu_seconds)
@@ -979,6 +1132,8 @@ def main():
         out["schedules"] = secondary
     if extras:
         out["configs"] = extras
+    if tuning:
+        out["tuning"] = tuning
     if rank == 0:
         sys.stdout.flush()
         os.write(result_fd, (json.dumps(out) + "\n").encode())

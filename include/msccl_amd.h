@@ -53,10 +53,14 @@ int mscclAmdPlanJson(const char* xmlFiles, int rank, int nranks, int coll, size_
  * same planning function as the communicator's (plan.cc: planCall) on the same inputs: the
  * schedules, the one-hop lowering and its size limit (co-resident: measured; across GPUs: the
  * link model), the Simple FIFO size, the fallback, the pair kernel (a one-pass
- * call of a schedule in pair form on every rank).  JSON {"kernel": "fold" | "pair" |
- * "interpreter" | "ring" | "tree", "algo", "proto", "lowered", "nBytes", "lowerMaxBytes",
- * "simpleBuffBytes", "remote", "pairForm", "classes": [fold orders per algorithm, 0 = not
- * lowered]}.  No GPU needed. */
+ * call of a schedule in pair form on every rank).  JSON {"kernel": "fold" | "pair" | "twophase" |
+ * "interpreter" | "ring" | "tree", "kernelExact", "algo", "proto", "lowered", "nBytes",
+ * "lowerMaxBytes", "simpleBuffBytes", "remote", "pairForm", "classes": [fold orders per
+ * algorithm, 0 = not lowered]}.  "kernelExact" is 0 when the answer for a multi-iteration
+ * pair-form call rests on the default FIFO and split (a non-default NCCL_LL_BUFFSIZE or a forced
+ * MSCCL_AMD_SPLIT: the communicator's one-pass bound follows its agreed split and FIFO geometry,
+ * which this call does not model).  The direct form (a launch holding every rank of a
+ * communicator) is not reported here: see mscclAmdDirectJson.  No GPU needed. */
 int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGpu, int coll, size_t count,
                            int dtype, int redop, int inPlace, char* out, size_t outLen);
 

@@ -238,16 +238,22 @@ int mscclAmdLaunchPlanJson(const char* xmlFiles, int rank, int nranks, int oneGp
   // an MSCCL call of a schedule in pair form on every rank runs the pair kernel on LL when it is one
   // pass and the knob is on (enqueue.cc: makeWork merges a pair-form call's iterations while a
   // workgroup's sends fit the FIFO: 64 iterations at the default LL FIFO and split 8, the bound
-  // used here)
+  // used here).  That bound is approximate for a multi-iteration call under a non-default
+  // NCCL_LL_BUFFSIZE or a forced MSCCL_AMD_SPLIT (the communicator's merge follows its agreed split
+  // and FIFO geometry): "kernelExact" is 0 for those answers.
   const bool pairCall = p.ringColl == 0 && p.algoIndex >= 0 && (size_t)p.algoIndex < pairAll.size() &&
                         pairAll[p.algoIndex] && p.proto == kProtoLL && k.pairKernel && k.smallKernel &&
                         (p.nIters <= 1 || (p.nIters <= 64 && p.sizePerChunk % std::max<int64_t>(1, p.chunkSize) == 0));
+  const bool pairMaybe = p.ringColl == 0 && p.algoIndex >= 0 && (size_t)p.algoIndex < pairAll.size() &&
+                         pairAll[p.algoIndex] && p.proto == kProtoLL && p.nIters > 1;
+  const bool exact = !(pairMaybe && (k.buffSizes[kProtoLL] != (int64_t)8 * 512 * kFifoSteps * 16 || k.split > 0));
   const char* kernel = p.ringColl == kTreeFlat ? (p.lowerMode == kLowerPair       ? "pair"
                                                   : p.lowerMode == kLowerTwoPhase ? "twophase"
                                                                                   : "fold")
                        : p.ringColl == kTreeAllReduce ? "tree" : p.ringColl ? "ring" : pairCall ? "pair" : "interpreter";
   std::ostringstream o;
-  o << "{\"kernel\":\"" << kernel << "\",\"algo\":" << p.algoIndex << ",\"proto\":" << p.proto
+  o << "{\"kernel\":\"" << kernel << "\",\"kernelExact\":" << (exact ? 1 : 0) << ",\"algo\":" << p.algoIndex
+    << ",\"proto\":" << p.proto
     << ",\"lowered\":" << (p.ringColl == kTreeFlat && p.algoIndex >= 0 ? 1 : 0) << ",\"nBytes\":" << p.nBytes
     << ",\"lowerMaxBytes\":" << (k.lowerMaxBytes >= 0 ? k.lowerMaxBytes : defaultLowerMaxBytes(nranks, c.remote))
     << ",\"simpleBuffBytes\":" << k.buffSizes[kProtoSimple] << ",\"remote\":" << (c.remote ? 1 : 0)

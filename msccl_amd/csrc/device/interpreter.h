@@ -2348,6 +2348,9 @@ __global__ void __launch_bounds__(kNT, 1) mscclTwoPhaseKernel(const LaunchArgsN<
 //                  store the result into every rank's output.
 // A lane reads every operand of a pack before it writes that pack anywhere, and no other lane
 // of the launch reads or writes it: in-place AllReduce calls are safe.
+#ifndef MSCCL_DIRECT_UD
+#define MSCCL_DIRECT_UD 4
+#endif
 struct alignas(16) DirectShared {
   const void* rankBuf[kMaxLaunchRanks];                // every rank's input, by rank
   uint8_t perm[kMaxDirectClasses][kMaxLaunchRanks];    // per class: the ranks in fold order
@@ -2359,7 +2362,7 @@ struct DirectRunner : Interp<T, OP, pSimple> {
   using I = Interp<T, OP, pSimple>;
   using I::PE;
   using F = typename I::F;
-  static constexpr int UD = 2;  // packs per lane per pass (n loads each in flight)
+  static constexpr int UD = MSCCL_DIRECT_UD;  // packs per lane per pass (n loads each in flight)
   // pack B of a block of n elements at a per-lane address (the rank whose operand a lane loads
   // follows its pack's chunk class, so a wave's lanes may read different ranks' buffers: no
   // wave-uniform buffer descriptor)

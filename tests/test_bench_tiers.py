@@ -43,6 +43,20 @@ def test_tier_spec_with_kinds(bench, tmp_path):
     assert [t[2] for t in tiers] == [1, 2, 4]
 
 
+def test_workload_label_names_the_schedule_that_ran(bench):
+    """config.workload names the headline size's schedule: "all-pairs" only on an all-pairs XML,
+    and the pair one-shot says it is not one."""
+    a = bench.workload_desc(False, 2, "LL", "fp32", kind="a")
+    assert a.startswith("C2: ") and "msccl-tools two-phase all-pairs XML" in a
+    p = bench.workload_desc(False, 2, "LL", "fp32", kind="p")
+    assert "pair one-shot" in p and "not all-pairs" in p
+    assert "all-pairs" not in p.replace("not all-pairs", "")
+    assert "C3 shape: " in bench.workload_desc(False, 8, "LL", "fp16", kind="a")
+    assert "over xGMI" in bench.workload_desc(True, 8, "LL", "fp16", kind="a")
+    assert "rehearsal" in bench.workload_desc(True, 8, "LL", "fp16", one_gpu=True, kind="O")
+    assert bench.parse(["--no-tuning"]).no_tuning
+
+
 def test_fused_pair_exchange_bytes(bench, tmp_path):
     """The roofline's algorithmic bytes: the pair exchange moves 7 S HBM bytes per rank unfused
     (s: S + 2S of LL lines, rrc: 2S + S + S) and 6 S when its s + rrc run fused (the source is

@@ -2,7 +2,8 @@
 
   C1  1 rank, fp32, 1 MiB: the nRanks == 1 copy (enqueue.cc:811-816)
   C2  2 ranks, LL, fp32, every sweep point 128 B .. 32 MiB, through bench.py's own size tiers
-      (one-shot x1 / one-shot x16 / two-phase all-pairs x16)
+      (the msccl-tools two-phase all-pairs XML, x1 below 4 KiB and x16 above, lowered at upload:
+      the fold up to 4 KiB, the pair exchange above)
   C3  8 ranks, LL, fp16, 128 B / 64 KiB / 1 MiB / 32 MiB: bench.py's 8-rank tiers and RCCL's
       32-tb all-pairs schedule with maxBytes raised (128 B takes the ring fallback there)
   C4  8 ranks, ring, Simple, bf16, 256 MiB per rank (bench.py's 32-ring schedule)

@@ -307,18 +307,38 @@ def test_pair_kernel_interoperates_with_other_kernels(peer, count, tmp_path):
 
 @pytest.mark.parametrize("nbytes", [128, 4092, 8192, 1 << 20, 32 << 20])
 def test_c2_tiers_take_the_pair_kernel(nbytes, tmp_path, monkeypatch):
-    """bench.py's C2 tiers with default settings: every one-pass size runs the pair kernel (small
-    calls included: the pair form is not lowered by default), the oracle's values."""
+    """The pair one-shot tiers (bench.PAIR_TIERS, C2's tiers in rounds 2-5) with default settings:
+    every one-pass size runs the pair kernel (small calls included: the pair form is not lowered by
+    default), the oracle's values."""
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
     monkeypatch.delenv("MSCCL_AMD_LOWER_MAX_BYTES", raising=False)
-    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path), bench.PAIR_TIERS)
     path = [t[3] for t in tiers if t[0] <= nbytes < t[1]][0]
     got, want, _ = run_collective(open(path).read(), 2, L.ALLREDUCE, nbytes // 4, 7, 0, True, seed=nbytes % 91,
                                   tmpdir=str(tmp_path))
     assert all(l["pair"] == 1 and l["ringColl"] == 0 for l in run_collective.last), run_collective.last
     _check(got, want, "C2 tier %d B" % nbytes)
+
+
+@pytest.mark.parametrize("nbytes", [128, 4080, 8192, 1 << 20, 32 << 20])
+def test_c2_default_tiers_run_the_allpairs_xml_lowered(nbytes, tmp_path, monkeypatch):
+    """bench.py's C2 tiers (the msccl-tools two-phase all-pairs XML): calls up to 4 KiB run the
+    one-hop fold, larger ones the pair exchange on the flat connections, with the values of the
+    schedule as written (oracle/sim.py runs the XML)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    monkeypatch.delenv("MSCCL_AMD_LOWER_MAX_BYTES", raising=False)
+    monkeypatch.delenv("MSCCL_AMD_LOWER_LARGE", raising=False)   # (this module's fixture sets it to 0)
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    path = [t[3] for t in tiers if t[0] <= nbytes < t[1]][0]
+    got, want, _ = run_collective(open(path).read(), 2, L.ALLREDUCE, nbytes // 4, 7, 0, True, seed=nbytes % 83,
+                                  tmpdir=str(tmp_path))
+    kernel = 2 if nbytes <= 4096 else 3
+    assert all(l["kernel"] == kernel and l["ringColl"] == 5 for l in run_collective.last), run_collective.last
+    _check(got, want, "C2 all-pairs tier %d B" % nbytes)
 
 
 def test_pair_tiers_long_mixed_sequence(tmp_path):
@@ -330,7 +350,7 @@ def test_pair_tiers_long_mixed_sequence(tmp_path):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path), bench.PAIR_TIERS)
     os.environ["MSCCL_XML_FILES"] = ":".join(t[3] for t in tiers)
     comms = M.Comm.init_all([0, 0])
     try:

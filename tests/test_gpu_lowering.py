@@ -50,7 +50,7 @@ def test_c2_pair_tiers_lowered(tmp_path, nbytes, monkeypatch):
     (by default 4 KiB for 2 ranks; 16 KiB here), the rest the pair kernel on the flat connections
     (a lowered large call), or with MSCCL_AMD_LOWER_LARGE=0 the exchange-set small kernel."""
     monkeypatch.setenv("MSCCL_AMD_LOWER_MAX_BYTES", str(16 << 10))
-    tiers = _bench().make_xmls(2, "LL", 16, str(tmp_path))
+    tiers = _bench().make_xmls(2, "LL", 16, str(tmp_path), _bench().PAIR_TIERS)
     for large in ("1", "0"):
         monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", large)
         with CoResident(2, [open(t[3]).read() for t in tiers], str(tmp_path)) as cr:
@@ -106,7 +106,9 @@ def test_knobs_and_limit(tmp_path, monkeypatch):
     monkeypatch.setenv("MSCCL_AMD_LOWER_LARGE", "0")
     with CoResident(2, [xml], str(tmp_path)) as cr:
         assert _case(cr, 1024, 7, 2)[0]["kernel"] == 2
-        assert _case(cr, 1028, 7, 3)[0]["kernel"] == 1
+        # not lowered: the schedule's own connections, the pair kernel (pair form, one pass)
+        last = _case(cr, 1028, 7, 3)[0]
+        assert last["kernel"] == 3 and last["ringColl"] == 0, last
 
 
 def test_lowered_interpreted_and_flat_calls_interleave(tmp_path, monkeypatch):

@@ -474,7 +474,7 @@ def test_four_processes_one_gpu_bench_tiers(tmp_path):
 
 
 # ------------------------------------------------------------------------------------------------
-# two ranks: bench.py --gpus 2 (C2: fp32, one rank per GPU, the pair exchange tiers)
+# two ranks: bench.py --gpus 2 (C2: fp32, one rank per GPU, the all-pairs XML tiers)
 
 def _two_rank_job(tmp_path, remote):
     b = _bench()
@@ -494,14 +494,14 @@ def _check_two(res, xmls, jobs):
 
 @needs2
 def test_two_processes_two_devices_c2_tiers(tmp_path):
-    """bench.py --gpus 2: 2 rank processes on 2 GPUs (hipIpc over xGMI), C2's tiers 128 B - 32 MiB:
-    the pair kernel at every size (a pair-form call merges into one pass), bit-exact
-    against the oracle."""
+    """bench.py --gpus 2: 2 rank processes on 2 GPUs (hipIpc over xGMI), C2's tiers 128 B - 32 MiB
+    (the two-phase all-pairs XML, lowered): the fold up to 4 KiB, the pair kernel on the flat
+    connections above, bit-exact against the oracle running the XML."""
     xmls, jobs = _two_rank_job(tmp_path, True)
     res = _eight_processes(tmp_path, xmls, jobs, world=2)
     _check_two(res, xmls, jobs)
     assert all(res[r][3] == 1 for r in range(2))
-    assert res[0][2] == [3, 3, 3, 3, 3], res[0][2]
+    assert res[0][2] == [2, 2, 3, 3, 3], res[0][2]
 
 
 def test_two_processes_one_gpu_forced_remote_c2_tiers(tmp_path):
@@ -511,4 +511,4 @@ def test_two_processes_one_gpu_forced_remote_c2_tiers(tmp_path):
     res = _eight_processes(tmp_path, xmls, jobs, world=2, one_gpu=True, env={"MSCCL_AMD_FORCE_REMOTE": "1"})
     _check_two(res, xmls, jobs)
     assert all(res[r][3] == 1 for r in range(2))
-    assert res[0][2] == [3, 3, 3, 3, 3], res[0][2]
+    assert res[0][2] == [2, 2, 3, 3, 3], res[0][2]

@@ -143,14 +143,28 @@ def test_pair_form_schedule_keeps_the_pair_kernel(tmp_path, monkeypatch):
 
 @pytest.mark.parametrize("nbytes", [128, 8192, 1 << 20, 32 << 20])
 def test_c2_tiers_launch_the_pair_kernel(tmp_path, nbytes):
-    """bench.py's C2 tiers: every size from 128 B to 32 MiB is a pair-form call that runs the pair
-    kernel in one pass, on one GPU and across GPUs; MSCCL_AMD_PAIR_KERNEL=0 leaves the interpreter."""
+    """The pair one-shot tiers (bench.PAIR_TIERS): every size from 128 B to 32 MiB is a pair-form
+    call that runs the pair kernel in one pass, on one GPU and across GPUs."""
     import bench
-    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path), bench.PAIR_TIERS)
     files = ":".join(t[3] for t in tiers)
     for one_gpu in (True, False):
         got = M.launch_plan_json(files, 0, 2, one_gpu, L.ALLREDUCE, nbytes // 4, 7, 0, True)
         assert got["kernel"] == "pair" and got["pairForm"] == 1, (one_gpu, got)
+
+
+@pytest.mark.parametrize("nbytes,kernel", [(128, "fold"), (4080, "fold"), (8192, "pair"), (1 << 20, "pair"),
+                                           (32 << 20, "pair")])
+def test_c2_default_tiers_run_the_allpairs_xml_lowered(tmp_path, nbytes, kernel):
+    """bench.py's C2 tiers (the msccl-tools two-phase all-pairs XML): lowered at every size, the
+    one-hop fold up to 4 KiB and the pair exchange on the flat connections above, either placement."""
+    import bench
+    tiers = bench.make_xmls(2, "LL", 16, str(tmp_path))
+    assert [t[4] for t in tiers] == ["a", "a"]
+    files = ":".join(t[3] for t in tiers)
+    for one_gpu in (True, False):
+        got = M.launch_plan_json(files, 0, 2, one_gpu, L.ALLREDUCE, nbytes // 4, 7, 0, True)
+        assert got["kernel"] == kernel and got["lowered"] == 1 and got["pairForm"] == 0, (one_gpu, got)
 
 
 def test_pair_kernel_knob_and_non_pair_schedules(tmp_path, monkeypatch):
@@ -178,3 +192,19 @@ def test_pair_kernel_knob_and_non_pair_schedules(tmp_path, monkeypatch):
     files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(1, "LL")])
     got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 24, 7, 0, True)
     assert got["kernel"] == "interpreter" and got["pairForm"] == 1, got
+    assert got["kernelExact"] == 1, got
+
+
+def test_pair_answer_flagged_approximate_off_the_default_fifo(tmp_path, monkeypatch):
+    """for a multi-iteration pair-form call the one-pass bound rests on the default LL
+    FIFO and split; under NCCL_LL_BUFFSIZE or MSCCL_AMD_SPLIT the answer says it is approximate."""
+    files = _files(tmp_path, [xmlgen.allreduce_pair_oneshot(1, "LL")])
+    got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 18, 7, 0, True)
+    assert got["kernelExact"] == 1, got
+    for env in (("NCCL_LL_BUFFSIZE", str(1 << 18)), ("MSCCL_AMD_SPLIT", "2")):
+        monkeypatch.setenv(*env)
+        got = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 1 << 18, 7, 0, True)
+        assert got["kernelExact"] == 0, (env, got)
+        small = M.launch_plan_json(files, 0, 2, True, L.ALLREDUCE, 32, 7, 0, True)
+        assert small["kernelExact"] == 1, (env, small)   # one iteration: exact
+        monkeypatch.delenv(env[0])
