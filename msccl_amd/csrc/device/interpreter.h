@@ -1403,6 +1403,7 @@ struct Interp {
     pinArgs(np, n, split, base, connSplit, tbStride, mode, images, sendG, recvG, epochs, sendbuff, recvbuff);
     constexpr int E = 8 / TS;
     constexpr int G = 8;  // peers per wait
+    static_assert(2 * G == 16, "ldLines16 takes 16 line addresses");
     const int npkAll = (n + PE - 1) / PE;
     // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges (the
     // first npkAll % split ranges one pack longer), cut into FIFO steps on its own sub-connection
@@ -1735,6 +1736,9 @@ struct Interp {
     void* const recvbuff = w.recvbuff;
     pinArgs(np, n, wgs, base, connSplit, tbStride, images, sendG, recvG, epochs, sendbuff, recvbuff);
     constexpr int G = 8;  // peers per wait / per batch of loads
+    // ldLines16 loads exactly 2 G lines: another G reads past la[] and ln[] (a variant built with
+    // G = 4 faulted the GPU, profiles/r06k_tp_occ.txt)
+    static_assert(2 * G == 16, "ldLines16 takes 16 line addresses");
     const int rem = M - base * wgs;
     const int p0 = wg * base + min(wg, rem);
     const int npk = base + (wg < rem ? 1 : 0);
