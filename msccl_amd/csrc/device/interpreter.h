@@ -2171,6 +2171,9 @@ struct PairRunner : Interp<T, OP, pLL> {
   // epoch and this lane's source packs of the first FIFO step (llFusedOp's cut), and the exchange
   // starts right after it.  The values, FIFO steps and flags are runSmall's (a peer may run either).
   __device__ __forceinline__ void run(const RankWork& w, int local) {
+#ifdef MSCCL_LAT_TRACE
+    const uint64_t tStart = __builtin_amdgcn_s_memrealtime();  // the measurement build's time origin
+#endif
     I& it = *this;
     it.tid = threadIdx.x;
     it.redArg = 0;
@@ -2236,8 +2239,29 @@ struct PairRunner : Interp<T, OP, pLL> {
     it.recvStep = uni(it.sh->rconn.step);
     it.headSeen = uni(it.sh->sconn.headSeen);
     it.tailSeen = uni(it.sh->rconn.tailSeen);
+#ifdef MSCCL_LAT_TRACE
+    // (tools/lat_trace.py: the same points as runSmall's, in this workgroup's trace slot)
+    it.trace = w.trace ? w.trace + (size_t)(bid * maxSplit + sub) * w.traceEvents : nullptr;
+    it.nev = 1;
+    it.maxEv = w.traceEvents;
+    it.ev(10, 0, 0);
+#endif
     [[clang::always_inline]] it.template llFusedOp<true, true>(src, dst, s, pre);
+#ifdef MSCCL_LAT_TRACE
+    it.ev(15, 0, 0);
+#endif
     it.epilogue(w, bid, sub, workIndex);
+#ifdef MSCCL_LAT_TRACE
+    it.ev(16, 0, 0);
+    if (it.trace != nullptr && it.tid == 0) {
+      TraceEvent e;
+      e.ts = tStart;
+      e.type = kEvHeader;
+      e.step = (uint16_t)it.nev;
+      e.arg = (uint32_t)workIndex;
+      it.trace[0] = e;
+    }
+#endif
   }
 };
 

@@ -4,7 +4,9 @@ AllReduces and prints, per trace point, the median time (us) from the workgroup'
   10 prologue done, 11 fused op entry, 12 first step's lines sent, 13 peer lines received and
   output stored, 14 head posted, 15 pass done, 16 epilogue done;
 then, over every workgroup of a launch, how far apart the workgroups started and ended (us).
-  MSCCL_AMD_LIB=tools/lat/libmsccl_amd_lat.so MSCCL_AMD_TRACE=2 python tools/lat_trace.py [bytes] [instances]"""
+  MSCCL_AMD_LIB=tools/lat/libmsccl_amd_lat.so MSCCL_AMD_TRACE=2 python tools/lat_trace.py [bytes] [instances]
+With LAT_TRACE_SCHEDULE=allpairs the pair kernel's points (PairRunner: 10 prologue done, 11-14 in
+the fused op, 15 op done, 16 epilogue done) of a lowered 2-rank all-pairs call (> 4 KiB)."""
 import os
 import sys
 
@@ -20,7 +22,12 @@ def main():
     nbytes = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     inst = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     path = "/tmp/lat_trace_%d.xml" % os.getpid()
-    open(path, "w").write(xmlgen.allreduce_pair_oneshot(inst, "LL"))
+    # LAT_TRACE_SCHEDULE=allpairs: the msccl-tools two-phase all-pairs (bench.py's C2 tiers), whose
+    # calls above 4 KiB run lowered on the pair kernel (PairRunner's trace points, same ids)
+    if os.environ.get("LAT_TRACE_SCHEDULE", "pair") == "allpairs":
+        open(path, "w").write(xmlgen.allreduce_allpairs(2, inst, "LL"))
+    else:
+        open(path, "w").write(xmlgen.allreduce_pair_oneshot(inst, "LL"))
     os.environ["MSCCL_XML_FILES"] = path
     comms = M.Comm.init_all([0, 0])
     cnt = nbytes // 4
