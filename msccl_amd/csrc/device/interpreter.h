@@ -1403,7 +1403,6 @@ struct Interp {
     pinArgs(np, n, split, base, connSplit, tbStride, mode, images, sendG, recvG, epochs, sendbuff, recvbuff);
     constexpr int E = 8 / TS;
     constexpr int G = 8;  // peers per wait
-    static_assert(2 * G == 16, "ldLines16 takes 16 line addresses");
     const int npkAll = (n + PE - 1) / PE;
     // this workgroup's packs: [p0, p0 + npk), the wg-th of RankWork::split contiguous ranges (the
     // first npkAll % split ranges one pack longer), cut into FIFO steps on its own sub-connection
@@ -1571,7 +1570,7 @@ struct Interp {
               la[2 * k + 1] = in + o1;
             }
             u32x4 ln[2 * G];
-            ldLines16(la, ln);
+            ldLinesPeers<G>(la, ln);
 #pragma unroll
             for (int k = 0; k < G; k++) {
               if (g0 + k >= np) continue;
@@ -1610,7 +1609,7 @@ struct Interp {
             la[2 * k + 1] = in + o1;
           }
           u32x4 ln[2 * G];
-          ldLines16(la, ln);
+          ldLinesPeers<G>(la, ln);
 #pragma unroll
           for (int k = 0; k < G; k++) {
             const int p = g0 + k;
@@ -1707,6 +1706,9 @@ struct Interp {
   // at once own disjoint packs: in-place calls are safe.  The three phases are software-pipelined
   // over the steps (below); no workgroup waits on a peer's step the peer has not reached, so the
   // loop cannot deadlock.
+#ifndef MSCCL_TP_OCC
+#define MSCCL_TP_OCC 1
+#endif
   static __device__ __forceinline__ uint32_t divQ(uint32_t m, uint32_t magic, int sh1, int sh2) {
     const uint32_t t = __umulhi(m, magic);
     return (t + ((m - t) >> sh1)) >> sh2;
@@ -1735,10 +1737,9 @@ struct Interp {
     const void* const sendbuff = w.sendbuff;
     void* const recvbuff = w.recvbuff;
     pinArgs(np, n, wgs, base, connSplit, tbStride, images, sendG, recvG, epochs, sendbuff, recvbuff);
-    constexpr int G = 8;  // peers per wait / per batch of loads
-    // ldLines16 loads exactly 2 G lines: another G reads past la[] and ln[] (a variant built with
-    // G = 4 faulted the GPU, profiles/r06k_tp_occ.txt)
-    static_assert(2 * G == 16, "ldLines16 takes 16 line addresses");
+    // peers per wait / per batch of loads: 8, or 4 in the build for two workgroups per CU
+    // (MSCCL_TP_OCC = 2, a measurement variant: <= 128 VGPRs)
+    constexpr int G = MSCCL_TP_OCC == 1 ? 8 : 4;
     const int rem = M - base * wgs;
     const int p0 = wg * base + min(wg, rem);
     const int npk = base + (wg < rem ? 1 : 0);
@@ -1884,7 +1885,7 @@ struct Interp {
               la[2 * k + 1] = in + o1;
             }
             u32x4 ln[2 * G];
-            ldLines16(la, ln);
+            ldLinesPeers<G>(la, ln);
 #pragma unroll
             for (int k = 0; k < G; k++) {
               const int p = g0 + k;
@@ -1931,7 +1932,7 @@ struct Interp {
               la[2 * k + 1] = in + o1;
             }
             u32x4 ln[2 * G];
-            ldLines16(la, ln);
+            ldLinesPeers<G>(la, ln);
 #pragma unroll
             for (int k = 0; k < G; k++) {
               if (g0 + k >= np) continue;
@@ -2350,8 +2351,10 @@ __global__ void __launch_bounds__(kNT, 1) mscclFoldKernel(const LaunchArgsN<R> a
 
 // The two-phase fold (Interp::runTwoPhase): rank r of the launch owns workgroups [blockBase,
 // blockBase + nBlocks), one per flat sub-connection.
+// MSCCL_TP_OCC: workgroups per CU the kernel is built for (1; 2: four waves per SIMD, <= 128
+// VGPRs, 4 peers per batch of loads; a measurement variant)
 template <typename T, int OP, int R>
-__global__ void __launch_bounds__(kNT, 1) mscclTwoPhaseKernel(const LaunchArgsN<R> args) {
+__global__ void __launch_bounds__(kNT, MSCCL_TP_OCC == 1 ? 1 : 4) mscclTwoPhaseKernel(const LaunchArgsN<R> args) {
   __shared__ BlockShared sh;
   __shared__ FoldShared fs;
   const int b = blockIdx.x;

@@ -182,6 +182,15 @@ __device__ __forceinline__ void ldLines16(const void* const* p, u32x4* x) {
         "v"(p[8]), "v"(p[9]), "v"(p[10]), "v"(p[11]), "v"(p[12]), "v"(p[13]), "v"(p[14]), "v"(p[15])
       : "memory");
 }
+// The fold kernels' batch: two lines of each of G peers in flight, one wait.  The array sizes are
+// part of the type, so a batch whose arrays do not hold exactly 2 G lines does not compile (a
+// variant that passed 8-entry arrays to ldLines16 read past them and faulted).
+template <int G>
+__device__ __forceinline__ void ldLinesPeers(const void* const (&p)[2 * G], u32x4 (&x)[2 * G]) {
+  static_assert(G == 4 || G == 8, "batches of 4 or 8 peers");
+  if constexpr (G == 8) ldLines16(p, x);
+  else ldLines8(p, x);
+}
 __device__ __forceinline__ void ldLine1(const void* a, u32x4& x) {
   asm volatile(
       "global_load_dwordx4 %0, %1, off sc0 sc1\n\t"
