@@ -57,6 +57,19 @@ def test_workload_label_names_the_schedule_that_ran(bench):
     assert bench.parse(["--no-tuning"]).no_tuning
 
 
+def test_secondary_lines_and_tuning_grid(bench):
+    """Beside a 2-rank headline (the all-pairs XML) the secondary line is the pair one-shot; at more
+    ranks the two-phase all-pairs x4 (and at N=1 RCCL's 8n-32tb file when installed).  The tuning
+    grid of bench.py --gpus N is the one DESIGN.md §6 / §10.4 names."""
+    two = bench.secondary_schedules(False, 2, 32 << 20)
+    assert two[0][0] == "pair_oneshot" and 'name="sec_pair"' in two[0][1], two[0][1][:200]
+    eight = bench.secondary_schedules(True, 8, 32 << 20)
+    assert [s[0] for s in eight] == ["allpairs_two_phase"]
+    assert bench.TUNE_SIZES == (64 << 10, 128 << 10, 256 << 10, 512 << 10, 1 << 20)
+    assert bench.TUNE_LOWER_CAPS == (128 << 10, 256 << 10, 512 << 10)
+    assert bench.TUNE_BUFFSIZES == (256 << 10, 4 << 20)
+
+
 def test_fused_pair_exchange_bytes(bench, tmp_path):
     """The roofline's algorithmic bytes: the pair exchange moves 7 S HBM bytes per rank unfused
     (s: S + 2S of LL lines, rrc: 2S + S + S) and 6 S when its s + rrc run fused (the source is
