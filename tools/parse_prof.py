@@ -36,7 +36,8 @@ def find(d, pattern):
 
 
 def is_msccl(name):
-    return any(k in name for k in ("mscclKernel", "mscclSmallKernel", "mscclFoldKernel", "mscclPairKernel"))
+    return any(k in name for k in ("mscclKernel", "mscclSmallKernel", "mscclFoldKernel", "mscclPairKernel",
+                                   "mscclTwoPhaseKernel", "mscclDirectKernel"))
 
 
 def counter_avg(d, counter):
