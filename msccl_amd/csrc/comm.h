@@ -90,6 +90,9 @@ struct ncclComm {
   };
   std::vector<DirectProgram> algoDirect;
   std::vector<msccl::DevAlgoHost> directAlgos;
+  // the ring fallback's Simple ReduceScatter as a direct form (one class: this rank's ring order
+  // r+1, r+2, ..., r, reduce_scatter.h:50-65); its AllGather needs no program
+  msccl::DevAlgoHost ringDirectRS;
   // communicators created together by one ncclCommInitAll with every rank on one device share a
   // nonzero clique id: a group call of all of them is one fused launch (the direct form's condition)
   uint64_t clique = 0;

@@ -266,9 +266,9 @@ RankWork makeFlatWork(Planned& p) {
 // RS 0.125 / 0.135 / 0.141, C4 0.809 / 0.802 / 0.935; profiles/r06g_c45_w*.json).
 RankWork makeDirectWork(Planned& p) {
   ncclComm* comm = p.op.comm;
-  const int g = p.plan.algoIndex;
-  const DevAlgoHost& da = comm->directAlgos[g];
-  const int coll = comm->algoDirect[g].coll;
+  const int g = p.plan.algoIndex;  // -1: the ring fallback's ReduceScatter / AllGather (plan.cc: planCall)
+  const DevAlgoHost& da = g >= 0 ? comm->directAlgos[g] : comm->ringDirectRS;
+  const int coll = g >= 0 ? comm->algoDirect[g].coll : p.plan.ringColl == kRingAllGather ? kAllGather : kReduceScatter;
   const int n = comm->nRanks;
   RankWork w;
   memset(&w, 0, sizeof(w));

@@ -375,6 +375,7 @@ ncclResult_t commFinish(ncclComm* comm) {
   pc.foldTwoPhase = &comm->foldTwoPhase;
   pc.directClasses = &comm->directClasses;
   pc.oneLaunch = comm->clique != 0;
+  pc.ringDirect = pc.oneLaunch && comm->knobs.direct && lowerOffered();
   pc.flat = flatEnabled(comm);
   pc.ringFallback = comm->ringFallback;
   pc.scratchSize = comm->scratchSize;
@@ -499,6 +500,7 @@ ncclResult_t commFree(ncclComm* comm, bool peerBarrier) {
     if (d.dImages) hipFree(d.dImages);  // the flat connections (comm->flatSend / flatRecv)
   for (auto& d : comm->directAlgos)
     if (d.dImages) hipFree(d.dImages);  // no connections
+  if (comm->ringDirectRS.dImages) hipFree(comm->ringDirectRS.dImages);
   if (comm->ringSend) hipFree(comm->ringSend);
   if (comm->ringRecv) hipFree(comm->ringRecv);
   if (comm->treeSend) hipFree(comm->treeSend);

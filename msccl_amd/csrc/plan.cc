@@ -471,6 +471,14 @@ int planCall(const PlanContext& ctx, const CallDesc& c, bool asyncMany, Plan* p)
   if (idx < 0) {
     // no MSCCL algorithm matches: the reference falls back to its ring (enqueue.cc:461-476)
     if (fallback()) {
+      // the ring's Simple ReduceScatter / AllGather on ranks that share one launch: the direct form
+      // (its values are the ring's: a block's fold along the ring from the rank after its owner,
+      // reduce_scatter.h:50-65; the AllGather's copies), decided at the launch (enqueue.cc)
+      if (ctx.ringDirect && k.direct && p->proto == kProtoSimple && c.redop <= kDevMin && p->nBytes <= (1ll << 30) &&
+          (p->ringColl == kRingReduceScatter || p->ringColl == kRingAllGather)) {
+        p->directOk = true;
+        p->directChunkPacks = 0;
+      }
       INFO(kSubColl, "MSCCL: no algorithm matches coll=%d count=%zu type=%d; %s fallback (%s, %d channels)", c.coll,
            c.count, c.dtype, p->ringColl == kTreeFlat ? "flat" : p->ringColl == kTreeAllReduce ? "tree" : "ring",
            p->proto == kProtoLL ? "LL" : "Simple", p->ringChannels);

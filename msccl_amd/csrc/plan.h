@@ -176,6 +176,8 @@ struct PlanContext {
   const std::vector<int>* foldTwoPhase = nullptr; // per algorithm: the lowering has a two-phase form
   const std::vector<int>* directClasses = nullptr; // per algorithm: the direct form's fold orders, 0: none
   bool oneLaunch = false;     // the communicator's group calls are one fused launch (ncclComm::clique)
+  bool ringDirect = false;    // oneLaunch, MSCCL_AMD_DIRECT and no trace / NPKit: the ring fallback's
+                              // Simple ReduceScatter / AllGather may run as the direct form
   bool flat = false;          // the flat group's connections exist (transport.cc: flatEnabled)
   bool ringFallback = true;   // MSCCL_AMD_RING_FALLBACK
   size_t scratchSize = 0;     // MSCCL scratch allocated at init

@@ -720,6 +720,30 @@ ncclResult_t algoUpload(ncclComm* comm) {
     putImage(img, 0, h, ts, none, none, reds);
     NCCLCHECK(uploadImages(img, &d));
   }
+  // the ring fallback's ReduceScatter (plan.cc: planCall): block b of the output is folded along
+  // the ring from rank b + 1 (its first `s`) to b (its `rrc`), reduce_scatter.h:50-65 with the ring
+  // in rank order; every chunk of the block alike, so one class and one chunk
+  if (comm->knobs.direct && comm->clique != 0) {
+    std::vector<int16_t> reds;
+    std::vector<Transfer> ts(2);
+    ts[0].srcoff = 1;
+    ts[0].redPtr = 0;
+    for (int j = 1; j <= comm->nRanks; j++) reds.push_back((int16_t)((comm->rank + j) % comm->nRanks));
+    ts[1].srcoff = 1;
+    ts[1].redPtr = (int16_t)reds.size();
+    reds.push_back(0);
+    DevAlgoHost& d = comm->ringDirectRS;
+    d.nBlocks = 1;
+    d.tbStride = (int)imageBytes(ts.size(), 0, reds.size());
+    std::vector<char> img((size_t)d.tbStride, 0);
+    DevTbHeader h;
+    memset(&h, 0, sizeof(h));
+    h.nsteps = (uint16_t)ts.size();
+    h.nreds = (uint16_t)reds.size();
+    const std::vector<int16_t> none;
+    putImage(img, 0, h, ts, none, none, reds);
+    NCCLCHECK(uploadImages(img, &d));
+  }
   return ringUpload(comm);
 }
 

@@ -109,3 +109,23 @@ def test_direct_knob_and_exact_c5_full_size(tmp_path, monkeypatch):
         assert all((l["kernel"] == 5) == (direct == "1") for l in run_collective.last), run_collective.last
     got, want, _ = run_collective(ag, 8, L.ALLGATHER, rc, 7, 0, False, seed=5, mode="exact", tmpdir=str(tmp_path))
     _check(got, want, "AG")
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("coll,count,dt,op", [(L.REDUCE_SCATTER, 300007, 7, 0), (L.REDUCE_SCATTER, 200003, 9, 2),
+                                              (L.REDUCE_SCATTER, 262147, 6, 3), (L.ALLGATHER, 300007, 6, 0),
+                                              (L.ALLGATHER, 777777, 0, 0)])
+@pytest.mark.parametrize("in_place", [True, False])
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_ring_fallback_direct(monkeypatch, n, coll, count, dt, op, in_place, direct):
+    """The ring fallback's Simple ReduceScatter / AllGather (no schedule loaded, ragged sizes above
+    the LL range) on ranks that share one launch: the direct form (a block folded along the ring
+    from the rank after its owner; the AllGather's copies), bit-exact against oracle/ring.py's
+    runRing; MSCCL_AMD_DIRECT=0 keeps the ring's FIFOs, the same bits."""
+    from tests.gpu_harness import run_ring_fallback
+    monkeypatch.setenv("MSCCL_AMD_DIRECT", direct)
+    gpu, ora, rp = run_ring_fallback(n, coll, count, dt, op, in_place, seed=count % 97)
+    assert (rp["last"]["kernel"] == 5) == (direct == "1"), rp["last"]
+    for r in range(n):
+        g, o = gpu[r].view(np.uint8), ora[r].view(np.uint8)
+        assert np.array_equal(g, o), "rank %d: %d differing bytes" % (r, int(np.count_nonzero(g != o)))
